@@ -1,0 +1,223 @@
+/*
+ * bls12_381_mi355x.h -- C ABI of the MI355X (gfx950) BLS12-381 prover hot path.
+ *
+ * This is the drop-in boundary.  Every entry point below replaces one exported by the
+ * reference backend (riusricardo/midnight-bls12-381-cuda, bls12-381/src/...) with the same
+ * name, argument meaning and error behaviour; the citation on each declaration is the
+ * reference definition it replaces.  Plain C: pointers, sizes, POD config structs, no C++ or
+ * torch types.  Streams are hipStream_t passed as void* (NULL = the default stream).
+ *
+ * Byte layouts (identical to blst / the reference, little-endian u64 limbs):
+ *   Fr          32 B   canonical, Montgomery (R = 2^256) unless a flag says standard
+ *   Fq          48 B   canonical, Montgomery (R = 2^384)
+ *   G1 affine   96 B   x || y;             identity = all zero
+ *   G2 affine  192 B   x.c0||x.c1||y.c0||y.c1; identity = all zero
+ *   G1 proj.   144 B   X || Y || Z          (meaning depends on the entry point, see below)
+ *   G2 proj.   288 B
+ */
+#ifndef BLS12_381_MI355X_H
+#define BLS12_381_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdbool.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------ */
+/* errors: ICICLE v4 numbering (reference include/icicle/errors.h:37-52).  The reference's
+ * own icicle_types.cuh:47-63 renumbers UNKNOWN_ERROR to 999; we follow real ICICLE.       */
+/* ------------------------------------------------------------------------------------ */
+typedef enum {
+    MBLS_SUCCESS = 0,
+    MBLS_INVALID_DEVICE = 1,
+    MBLS_OUT_OF_MEMORY = 2,
+    MBLS_INVALID_POINTER = 3,
+    MBLS_ALLOCATION_FAILED = 4,
+    MBLS_DEALLOCATION_FAILED = 5,
+    MBLS_COPY_FAILED = 6,
+    MBLS_SYNCHRONIZATION_FAILED = 7,
+    MBLS_STREAM_CREATION_FAILED = 8,
+    MBLS_STREAM_DESTRUCTION_FAILED = 9,
+    MBLS_API_NOT_IMPLEMENTED = 10,
+    MBLS_INVALID_ARGUMENT = 11,
+    MBLS_BACKEND_LOAD_FAILED = 12,
+    MBLS_LICENSE_CHECK_ERROR = 13,
+    MBLS_UNKNOWN_ERROR = 14
+} eIcicleError;
+
+/* ------------------------------------------------------------------------------------ */
+/* element types (opaque byte containers with the layouts above)                         */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { uint64_t limbs[4]; } mbls_fr_t;
+typedef struct { uint64_t limbs[6]; } mbls_fq_t;
+typedef struct { mbls_fq_t c0, c1; } mbls_fq2_t;
+typedef struct { mbls_fq_t x, y; } mbls_g1_affine_t;
+typedef struct { mbls_fq_t x, y, z; } mbls_g1_projective_t;
+typedef struct { mbls_fq2_t x, y; } mbls_g2_affine_t;
+typedef struct { mbls_fq2_t x, y, z; } mbls_g2_projective_t;
+
+/* ------------------------------------------------------------------------------------ */
+/* configs: byte-compatible with ICICLE v4 (reference icicle_types.cuh:102-201)           */
+/* ------------------------------------------------------------------------------------ */
+typedef enum { MBLS_NTT_FORWARD = 0, MBLS_NTT_INVERSE = 1 } NTTDir;   /* icicle_types.cuh:83-86 */
+typedef enum {                                                      /* icicle_types.cuh:88-95 */
+    MBLS_ORDERING_NN = 0, MBLS_ORDERING_NR = 1, MBLS_ORDERING_RN = 2,
+    MBLS_ORDERING_RR = 3, MBLS_ORDERING_NM = 4, MBLS_ORDERING_MN = 5
+} Ordering;
+
+/* MSMConfig -- icicle_types.cuh:155-169 */
+typedef struct {
+    void* stream;
+    int precompute_factor;
+    int c;                            /* window bits, 0 = auto                         */
+    int bitsize;                      /* scalar bits, 0 = 255                          */
+    int batch_size;                   /* number of MSMs (scalars/results are batched)   */
+    bool are_points_shared_in_batch;
+    bool are_scalars_on_device;
+    bool are_scalars_montgomery_form;
+    bool are_points_on_device;
+    bool are_points_montgomery_form;
+    bool are_results_on_device;
+    bool is_async;
+    void* ext;
+} MSMConfig;
+
+/* NTTConfig<Fr> -- icicle_types.cuh:102-113 (coset_gen is a 32-byte Fr) */
+typedef struct {
+    void* stream;
+    mbls_fr_t coset_gen;
+    int batch_size;
+    bool columns_batch;
+    Ordering ordering;
+    bool are_inputs_on_device;
+    bool are_outputs_on_device;
+    bool is_async;
+    void* ext;
+} NTTConfig;
+
+/* NTTInitDomainConfig -- icicle_types.cuh:136-140 */
+typedef struct {
+    void* stream;
+    bool is_async;
+    void* ext;
+} NTTInitDomainConfig;
+
+/* VecOpsConfig -- ICICLE v4 layout (icicle_types.cuh:194-201 plus v4's batch fields,
+ * which core/vecops.rs:346 sets) */
+typedef struct {
+    void* stream;
+    bool is_a_on_device;
+    bool is_b_on_device;
+    bool is_result_on_device;
+    bool is_async;
+    int batch_size;
+    bool columns_batch;
+    void* ext;
+} VecOpsConfig;
+
+MSMConfig mbls_default_msm_config(void);
+NTTConfig mbls_default_ntt_config(void);
+VecOpsConfig mbls_default_vec_ops_config(void);
+
+/* ------------------------------------------------------------------------------------ */
+/* MSM                                                                                    */
+/* ------------------------------------------------------------------------------------ */
+/* Raw kernel-level MSM, reference icicle_curve_api.cu:679-705 (bls12_381_g1_msm_cuda /
+ * bls12_381_g2_msm_cuda -> msm::msm_cuda, msm_kernels.cu:603-903):
+ *   scalars STANDARD form, bases Montgomery affine, result = Jacobian Montgomery point
+ *   (identity: Z = 0).  Host/device placement from config->are_*_on_device.           */
+eIcicleError bls12_381_g1_msm_cuda(const mbls_fr_t* scalars, const mbls_g1_affine_t* bases, int msm_size,
+                                   const MSMConfig* config, mbls_g1_projective_t* result);
+eIcicleError bls12_381_g2_msm_cuda(const mbls_fr_t* scalars, const mbls_g2_affine_t* bases, int msm_size,
+                                   const MSMConfig* config, mbls_g2_projective_t* result);
+
+/* ICICLE-registered MSM semantics, reference icicle_curve_api.cu:243-407 (msm_cuda_impl) and
+ * :454-618 (msm_g2_cuda_impl): honours are_scalars_montgomery_form /
+ * are_points_montgomery_form, returns ICICLE standard-form projective (x, y, 1) with
+ * identity (0, 1, 0).  batch_size > 1 computes batch_size MSMs (the reference silently
+ * computes only the first, SURVEY.md finding 3): scalars are batch_size*msm_size, bases are
+ * msm_size (shared) or batch_size*msm_size, results batch_size.                          */
+eIcicleError bls12_381_icicle_g1_msm(const mbls_fr_t* scalars, const mbls_g1_affine_t* bases, int msm_size,
+                                     const MSMConfig* config, mbls_g1_projective_t* results);
+eIcicleError bls12_381_icicle_g2_msm(const mbls_fr_t* scalars, const mbls_g2_affine_t* bases, int msm_size,
+                                     const MSMConfig* config, mbls_g2_projective_t* results);
+
+/* precompute_bases, reference icicle_curve_api.cu:415-440: factor 1 only (byte copy);
+ * factor > 1 returns MBLS_API_NOT_IMPLEMENTED rather than silently wrong data.           */
+eIcicleError bls12_381_icicle_g1_msm_precompute_bases(const mbls_g1_affine_t* input_bases, int bases_size,
+                                                      const MSMConfig* config, mbls_g1_affine_t* output_bases);
+eIcicleError bls12_381_icicle_g2_msm_precompute_bases(const mbls_g2_affine_t* input_bases, int bases_size,
+                                                      const MSMConfig* config, mbls_g2_affine_t* output_bases);
+
+/* ------------------------------------------------------------------------------------ */
+/* NTT (reference ntt_kernels.cu:1907-1943, icicle_field_api.cu:363-383)                  */
+/* Semantics follow the CPU path (core/ntt.rs:1488-1603, best_fft): forward
+ * out_j = sum_i in_i w^(ij), inverse = n^-1 sum_j in_j w^(-ij), w = ROOT_OF_UNITY^(2^(32-k))
+ * for size 2^k, natural order in and out (kNN).                                          */
+/* ------------------------------------------------------------------------------------ */
+eIcicleError bls12_381_ntt_init_domain_cuda(const mbls_fr_t* root_of_unity, const NTTInitDomainConfig* config);
+eIcicleError bls12_381_ntt_release_domain_cuda(void);
+eIcicleError bls12_381_ntt_cuda(const mbls_fr_t* input, int size, NTTDir dir, const NTTConfig* config,
+                                mbls_fr_t* output);
+eIcicleError bls12_381_coset_ntt_cuda(const mbls_fr_t* input, int size, NTTDir dir, const mbls_fr_t* coset_gen,
+                                      const NTTConfig* config, mbls_fr_t* output);
+eIcicleError bls12_381_field_ntt_cuda(const mbls_fr_t* input, int size, NTTDir dir, const NTTConfig* config,
+                                      mbls_fr_t* output);
+eIcicleError bls12_381_field_ntt_init_domain_cuda(const mbls_fr_t* root_of_unity, const NTTInitDomainConfig* config);
+eIcicleError bls12_381_field_ntt_release_domain_cuda(void);
+
+/* ------------------------------------------------------------------------------------ */
+/* vecops (reference vec_ops.cu:393-524 and :693-840; icicle_field_api.cu:194-334)        */
+/* raw-limb semantics: add/sub representation-agnostic, mul = Montgomery product.         */
+/* ------------------------------------------------------------------------------------ */
+eIcicleError bls12_381_vector_add(const mbls_fr_t* a, const mbls_fr_t* b, size_t size, const VecOpsConfig* config,
+                                  mbls_fr_t* output);
+eIcicleError bls12_381_vector_sub(const mbls_fr_t* a, const mbls_fr_t* b, size_t size, const VecOpsConfig* config,
+                                  mbls_fr_t* output);
+eIcicleError bls12_381_vector_mul(const mbls_fr_t* a, const mbls_fr_t* b, size_t size, const VecOpsConfig* config,
+                                  mbls_fr_t* output);
+/* scalar_{mul,add}_vec: `scalar` is ONE element on the host unless config->is_a_on_device
+ * (icicle_field_api.cu:227-334). */
+eIcicleError bls12_381_scalar_mul_vec(const mbls_fr_t* scalar, const mbls_fr_t* vec, size_t size,
+                                      const VecOpsConfig* config, mbls_fr_t* output);
+eIcicleError bls12_381_scalar_add_vec(const mbls_fr_t* scalar, const mbls_fr_t* vec, size_t size,
+                                      const VecOpsConfig* config, mbls_fr_t* output);
+/* device-pointer kernel entry points, vec_ops.cu:393-476 (output first, device pointers;
+ * `scalar` is a HOST pointer to one element as in the reference). */
+eIcicleError vec_add_cuda(mbls_fr_t* output, const mbls_fr_t* a, const mbls_fr_t* b, int size, const VecOpsConfig* config);
+eIcicleError vec_sub_cuda(mbls_fr_t* output, const mbls_fr_t* a, const mbls_fr_t* b, int size, const VecOpsConfig* config);
+eIcicleError vec_mul_cuda(mbls_fr_t* output, const mbls_fr_t* a, const mbls_fr_t* b, int size, const VecOpsConfig* config);
+eIcicleError scalar_mul_vec_cuda(mbls_fr_t* output, const mbls_fr_t* scalar, const mbls_fr_t* vec, int size,
+                                 const VecOpsConfig* config);
+eIcicleError scalar_add_vec_cuda(mbls_fr_t* output, const mbls_fr_t* scalar, const mbls_fr_t* vec, int size,
+                                 const VecOpsConfig* config);
+
+/* ------------------------------------------------------------------------------------ */
+/* library utilities (no reference counterpart; used by the host API, tests and bench)   */
+/* ------------------------------------------------------------------------------------ */
+const char* mbls_version(void);
+const char* mbls_error_string(eIcicleError e);
+/* Fill `out` (device) with n synthetic scalars of stream `seed` (standard form if
+ * montgomery == false).  Same stream as the oracle's orc_gen_scalars. */
+eIcicleError mbls_gen_scalars(mbls_fr_t* out_device, uint64_t seed, size_t n, bool montgomery, void* stream);
+/* Fill `out` (device) with P_i = k_i * G, k_i = scalar stream `seed` (affine Montgomery). */
+eIcicleError mbls_gen_g1_bases(mbls_g1_affine_t* out_device, uint64_t seed, size_t n, void* stream);
+eIcicleError mbls_gen_g2_bases(mbls_g2_affine_t* out_device, uint64_t seed, size_t n, void* stream);
+/* Sum `count` Jacobian-Montgomery points on device (the EC reduction after the multi-GPU
+ * all-gather of partial MSM results). result: device pointer, Jacobian Montgomery. */
+eIcicleError mbls_g1_sum_jacobian(const mbls_g1_projective_t* points_device, int count,
+                                  mbls_g1_projective_t* result_device, void* stream);
+eIcicleError mbls_g2_sum_jacobian(const mbls_g2_projective_t* points_device, int count,
+                                  mbls_g2_projective_t* result_device, void* stream);
+/* Jacobian Montgomery -> ICICLE standard projective (x, y, 1) / (0, 1, 0), in place on
+ * device (reference icicle_curve_api.cu:134-229). */
+eIcicleError mbls_g1_jacobian_to_icicle(mbls_g1_projective_t* points_device, int count, void* stream);
+eIcicleError mbls_g2_jacobian_to_icicle(mbls_g2_projective_t* points_device, int count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLS12_381_MI355X_H */

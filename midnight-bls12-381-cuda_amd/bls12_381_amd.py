@@ -1,0 +1,289 @@
+"""ctypes binding of libbls12_381_mi355x.so (the C ABI in include/bls12_381_mi355x.h).
+
+Thin: config structs, error mapping, and numpy/torch conveniences for tests and bench.
+There is no CPU fallback -- if the HIP library is missing or fails to load this module raises.
+Device buffers are torch tensors (torch is plumbing here: allocation + streams)."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libbls12_381_mi355x.so")
+
+ERRORS = ["SUCCESS", "INVALID_DEVICE", "OUT_OF_MEMORY", "INVALID_POINTER", "ALLOCATION_FAILED",
+          "DEALLOCATION_FAILED", "COPY_FAILED", "SYNCHRONIZATION_FAILED", "STREAM_CREATION_FAILED",
+          "STREAM_DESTRUCTION_FAILED", "API_NOT_IMPLEMENTED", "INVALID_ARGUMENT", "BACKEND_LOAD_FAILED",
+          "LICENSE_CHECK_ERROR", "UNKNOWN_ERROR"]
+SUCCESS, INVALID_POINTER, API_NOT_IMPLEMENTED, INVALID_ARGUMENT = 0, 3, 10, 11
+
+
+class IcicleError(RuntimeError):
+    def __init__(self, code, what):
+        name = ERRORS[code] if 0 <= code < len(ERRORS) else str(code)
+        super().__init__(f"{what} failed: {name} ({code})")
+        self.code = code
+
+
+class MSMConfig(ctypes.Structure):
+    _fields_ = [("stream", ctypes.c_void_p), ("precompute_factor", ctypes.c_int), ("c", ctypes.c_int),
+                ("bitsize", ctypes.c_int), ("batch_size", ctypes.c_int),
+                ("are_points_shared_in_batch", ctypes.c_bool), ("are_scalars_on_device", ctypes.c_bool),
+                ("are_scalars_montgomery_form", ctypes.c_bool), ("are_points_on_device", ctypes.c_bool),
+                ("are_points_montgomery_form", ctypes.c_bool), ("are_results_on_device", ctypes.c_bool),
+                ("is_async", ctypes.c_bool), ("ext", ctypes.c_void_p)]
+
+
+class FrC(ctypes.Structure):
+    _fields_ = [("limbs", ctypes.c_uint64 * 4)]
+
+
+class NTTConfig(ctypes.Structure):
+    _fields_ = [("stream", ctypes.c_void_p), ("coset_gen", FrC), ("batch_size", ctypes.c_int),
+                ("columns_batch", ctypes.c_bool), ("ordering", ctypes.c_int),
+                ("are_inputs_on_device", ctypes.c_bool), ("are_outputs_on_device", ctypes.c_bool),
+                ("is_async", ctypes.c_bool), ("ext", ctypes.c_void_p)]
+
+
+class NTTInitDomainConfig(ctypes.Structure):
+    _fields_ = [("stream", ctypes.c_void_p), ("is_async", ctypes.c_bool), ("ext", ctypes.c_void_p)]
+
+
+class VecOpsConfig(ctypes.Structure):
+    _fields_ = [("stream", ctypes.c_void_p), ("is_a_on_device", ctypes.c_bool), ("is_b_on_device", ctypes.c_bool),
+                ("is_result_on_device", ctypes.c_bool), ("is_async", ctypes.c_bool), ("batch_size", ctypes.c_int),
+                ("columns_batch", ctypes.c_bool), ("ext", ctypes.c_void_p)]
+
+
+# every symbol include/bls12_381_mi355x.h declares (checked by tests/test_abi.py)
+EXPORTED = [
+    "mbls_default_msm_config", "mbls_default_ntt_config", "mbls_default_vec_ops_config",
+    "bls12_381_g1_msm_cuda", "bls12_381_g2_msm_cuda", "bls12_381_icicle_g1_msm", "bls12_381_icicle_g2_msm",
+    "bls12_381_icicle_g1_msm_precompute_bases", "bls12_381_icicle_g2_msm_precompute_bases",
+    "bls12_381_ntt_init_domain_cuda", "bls12_381_ntt_release_domain_cuda", "bls12_381_ntt_cuda",
+    "bls12_381_coset_ntt_cuda", "bls12_381_field_ntt_cuda", "bls12_381_field_ntt_init_domain_cuda",
+    "bls12_381_field_ntt_release_domain_cuda",
+    "bls12_381_vector_add", "bls12_381_vector_sub", "bls12_381_vector_mul", "bls12_381_scalar_mul_vec",
+    "bls12_381_scalar_add_vec", "vec_add_cuda", "vec_sub_cuda", "vec_mul_cuda", "scalar_mul_vec_cuda",
+    "scalar_add_vec_cuda",
+    "mbls_version", "mbls_error_string", "mbls_gen_scalars", "mbls_gen_g1_bases", "mbls_gen_g2_bases",
+    "mbls_g1_sum_jacobian", "mbls_g2_sum_jacobian", "mbls_g1_jacobian_to_icicle", "mbls_g2_jacobian_to_icicle",
+]
+
+_LIB = None
+
+
+def lib():
+    """Load the HIP library (raises if it is missing: there is no fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    P, E = ctypes.c_void_p, ctypes.c_int
+    sz, i32, u64, b = ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64, ctypes.c_bool
+    sig = {
+        "bls12_381_g1_msm_cuda": [P, P, i32, P, P], "bls12_381_g2_msm_cuda": [P, P, i32, P, P],
+        "bls12_381_icicle_g1_msm": [P, P, i32, P, P], "bls12_381_icicle_g2_msm": [P, P, i32, P, P],
+        "bls12_381_icicle_g1_msm_precompute_bases": [P, i32, P, P],
+        "bls12_381_icicle_g2_msm_precompute_bases": [P, i32, P, P],
+        "bls12_381_ntt_init_domain_cuda": [P, P], "bls12_381_ntt_release_domain_cuda": [],
+        "bls12_381_ntt_cuda": [P, i32, i32, P, P], "bls12_381_coset_ntt_cuda": [P, i32, i32, P, P, P],
+        "bls12_381_field_ntt_cuda": [P, i32, i32, P, P], "bls12_381_field_ntt_init_domain_cuda": [P, P],
+        "bls12_381_field_ntt_release_domain_cuda": [],
+        "bls12_381_vector_add": [P, P, sz, P, P], "bls12_381_vector_sub": [P, P, sz, P, P],
+        "bls12_381_vector_mul": [P, P, sz, P, P], "bls12_381_scalar_mul_vec": [P, P, sz, P, P],
+        "bls12_381_scalar_add_vec": [P, P, sz, P, P],
+        "vec_add_cuda": [P, P, P, i32, P], "vec_sub_cuda": [P, P, P, i32, P], "vec_mul_cuda": [P, P, P, i32, P],
+        "scalar_mul_vec_cuda": [P, P, P, i32, P], "scalar_add_vec_cuda": [P, P, P, i32, P],
+        "mbls_gen_scalars": [P, u64, sz, b, P], "mbls_gen_g1_bases": [P, u64, sz, P],
+        "mbls_gen_g2_bases": [P, u64, sz, P], "mbls_g1_sum_jacobian": [P, i32, P, P],
+        "mbls_g2_sum_jacobian": [P, i32, P, P], "mbls_g1_jacobian_to_icicle": [P, i32, P],
+        "mbls_g2_jacobian_to_icicle": [P, i32, P],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = E
+    L.mbls_version.restype = ctypes.c_char_p
+    L.mbls_error_string.restype = ctypes.c_char_p
+    L.mbls_error_string.argtypes = [E]
+    L.mbls_default_msm_config.restype = MSMConfig
+    L.mbls_default_ntt_config.restype = NTTConfig
+    L.mbls_default_vec_ops_config.restype = VecOpsConfig
+    _LIB = L
+    return L
+
+
+def check(code, what):
+    if code != SUCCESS:
+        raise IcicleError(code, what)
+
+
+def _p(x):
+    """pointer of a numpy array or torch tensor"""
+    if x is None:
+        return None
+    if isinstance(x, np.ndarray):
+        assert x.flags["C_CONTIGUOUS"]
+        return ctypes.c_void_p(x.ctypes.data)
+    return ctypes.c_void_p(x.data_ptr())
+
+
+def _is_dev(x):
+    return x is not None and not isinstance(x, np.ndarray)
+
+
+def _stream_handle(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+# ----------------------------------------------------------------------------- configs
+def msm_config(**kw):
+    c = lib().mbls_default_msm_config()
+    for k, v in kw.items():
+        if k == "stream":
+            c.stream = _stream_handle(v)
+        else:
+            setattr(c, k, v)
+    return c
+
+
+def ntt_config(**kw):
+    c = lib().mbls_default_ntt_config()
+    for k, v in kw.items():
+        if k == "stream":
+            c.stream = _stream_handle(v)
+        elif k == "coset_gen":
+            for i in range(4):
+                c.coset_gen.limbs[i] = int(v[i])
+        else:
+            setattr(c, k, v)
+    return c
+
+
+def vec_config(**kw):
+    c = lib().mbls_default_vec_ops_config()
+    for k, v in kw.items():
+        if k == "stream":
+            c.stream = _stream_handle(v)
+        else:
+            setattr(c, k, v)
+    return c
+
+
+# ----------------------------------------------------------------------------- vecops
+_VEC = {"add": "bls12_381_vector_add", "sub": "bls12_381_vector_sub", "mul": "bls12_381_vector_mul",
+        "scalar_mul": "bls12_381_scalar_mul_vec", "scalar_add": "bls12_381_scalar_add_vec"}
+
+
+def vec_op(op, a, b, out=None, stream=None, is_async=False):
+    """a, b: (n,4) uint64 numpy (host) or torch (device) arrays; for scalar ops `a` is one
+    element (host numpy (4,) unless it is a device tensor)."""
+    n = b.shape[0]
+    if out is None:
+        out = np.zeros((n, 4), dtype=np.uint64)
+    cfg = vec_config(is_a_on_device=_is_dev(a), is_b_on_device=_is_dev(b), is_result_on_device=_is_dev(out),
+                     is_async=is_async, stream=stream)
+    check(getattr(lib(), _VEC[op])(_p(a), _p(b), n, ctypes.byref(cfg), _p(out)), _VEC[op])
+    return out
+
+
+# ----------------------------------------------------------------------------- NTT
+def ntt_init_domain(root_mont=None):
+    if root_mont is None:  # canonical 2^32-th root, Montgomery form
+        root_mont = np.array([0xb9b58d8c5f0e466a, 0x5b1b4c801819d7ec, 0x0af53ae352a31e64, 0x5bf3adda19e9b27b],
+                             dtype=np.uint64)
+    cfg = NTTInitDomainConfig()
+    check(lib().bls12_381_ntt_init_domain_cuda(_p(np.ascontiguousarray(root_mont, dtype=np.uint64)),
+                                               ctypes.byref(cfg)), "ntt_init_domain")
+
+
+def ntt(x, inverse=False, out=None, batch=1, stream=None, is_async=False, coset_gen=None):
+    """x: (batch*n, 4) uint64 numpy (host) or torch (device)."""
+    total = x.shape[0]
+    n = total // batch
+    if out is None:
+        out = np.zeros((total, 4), dtype=np.uint64) if isinstance(x, np.ndarray) else None
+    kw = dict(batch_size=batch, are_inputs_on_device=_is_dev(x), are_outputs_on_device=_is_dev(out),
+              is_async=is_async, stream=stream)
+    if coset_gen is not None:
+        kw["coset_gen"] = coset_gen
+    cfg = ntt_config(**kw)
+    check(lib().bls12_381_ntt_cuda(_p(x), n, 1 if inverse else 0, ctypes.byref(cfg), _p(out)), "ntt")
+    return out
+
+
+# ----------------------------------------------------------------------------- MSM
+def msm(group, scalars, bases, *, icicle=True, scalars_mont=False, points_mont=True, c=0, bitsize=0,
+        precompute_factor=1, batch=1, shared_bases=True, out=None, stream=None, is_async=False, n=None):
+    """scalars (batch*n, 4) u64, bases (n*F[*batch], 12|24) u64; host numpy or device torch.
+    icicle=True -> ICICLE semantics (standard (x, y, 1)); False -> raw Jacobian Montgomery."""
+    nl = 18 if group == "g1" else 36
+    if n is None:
+        n = scalars.shape[0] // batch
+    if out is None:
+        out = np.zeros((batch, nl), dtype=np.uint64)
+    cfg = msm_config(c=c, bitsize=bitsize, precompute_factor=precompute_factor, batch_size=batch,
+                     are_points_shared_in_batch=shared_bases, are_scalars_on_device=_is_dev(scalars),
+                     are_scalars_montgomery_form=scalars_mont, are_points_on_device=_is_dev(bases),
+                     are_points_montgomery_form=points_mont, are_results_on_device=_is_dev(out),
+                     is_async=is_async, stream=stream)
+    if icicle:
+        fn = lib().bls12_381_icicle_g1_msm if group == "g1" else lib().bls12_381_icicle_g2_msm
+    else:
+        fn = lib().bls12_381_g1_msm_cuda if group == "g1" else lib().bls12_381_g2_msm_cuda
+    check(fn(_p(scalars), _p(bases), n, ctypes.byref(cfg), _p(out)), f"{group} msm")
+    return out
+
+
+def precompute_bases(group, bases, factor, n, c=0, out=None):
+    nl = 12 if group == "g1" else 24
+    if out is None:
+        out = np.zeros((n * factor, nl), dtype=np.uint64)
+    cfg = msm_config(precompute_factor=factor, c=c, are_points_on_device=_is_dev(bases),
+                     are_points_montgomery_form=True, are_results_on_device=_is_dev(out))
+    fn = (lib().bls12_381_icicle_g1_msm_precompute_bases if group == "g1"
+          else lib().bls12_381_icicle_g2_msm_precompute_bases)
+    check(fn(_p(bases), n, ctypes.byref(cfg), _p(out)), "precompute_bases")
+    return out
+
+
+# ----------------------------------------------------------------------------- utilities
+def gen_scalars(out_dev, seed, montgomery=False, stream=None):
+    check(lib().mbls_gen_scalars(_p(out_dev), seed, out_dev.shape[0], montgomery, _stream_handle(stream)),
+          "gen_scalars")
+
+
+def gen_bases(group, out_dev, seed, stream=None):
+    fn = lib().mbls_gen_g1_bases if group == "g1" else lib().mbls_gen_g2_bases
+    check(fn(_p(out_dev), seed, out_dev.shape[0], _stream_handle(stream)), "gen_bases")
+
+
+def sum_jacobian(group, pts_dev, out_dev, stream=None):
+    fn = lib().mbls_g1_sum_jacobian if group == "g1" else lib().mbls_g2_sum_jacobian
+    check(fn(_p(pts_dev), pts_dev.shape[0], _p(out_dev), _stream_handle(stream)), "sum_jacobian")
+
+
+def jacobian_to_icicle(group, pts_dev, stream=None):
+    fn = lib().mbls_g1_jacobian_to_icicle if group == "g1" else lib().mbls_g2_jacobian_to_icicle
+    check(fn(_p(pts_dev), pts_dev.shape[0], _stream_handle(stream)), "jacobian_to_icicle")
+
+
+def torch_u64(shape_or_array, device="cuda"):
+    """uint64 limb storage on the device (int64 dtype: torch is only the allocator)."""
+    import torch
+    if isinstance(shape_or_array, np.ndarray):
+        return torch.from_numpy(shape_or_array.view(np.int64)).to(device)
+    return torch.zeros(shape_or_array, dtype=torch.int64, device=device)
+
+
+def to_numpy_u64(t):
+    return t.detach().cpu().numpy().view(np.uint64)

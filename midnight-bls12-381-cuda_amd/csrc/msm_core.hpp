@@ -1,0 +1,531 @@
+// msm_core.hpp -- Pippenger multi-scalar multiplication over G1 / G2 for CDNA4 (templates).
+//
+// Reference: orchestration msm::msm_cuda (bls12-381/src/curve/msm_kernels.cu:603-903),
+// digits compute_bucket_indices_kernel (:69-143), histogram (:224-256), cub scan+sort
+// (:748-781), accumulation (:269-366), bucket reduction (:376-513), final (:529-596);
+// boundary msm_cuda_impl / msm_g2_cuda_impl (icicle_curve_api.cu:243-618).
+//
+// Pipeline (all on the caller's stream, scratch from the per-stream arena):
+//   1. k_digits       (msm_common.hip) one thread per scalar: Montgomery -> standard if
+//                     flagged, signed c-bit digits, (key, index|sign) pairs window-major,
+//                     bucket histogram by atomics.
+//   2. scans          bucket offsets; buckets are split in chunks of <= CHUNK points so one
+//                     heavy bucket (e.g. all-equal scalars) cannot serialise a thread.
+//   3. k_scatter      counting-sort scatter (keys < TB: no radix sort needed).
+//   4. k_accumulate   one thread per chunk: sum of +-P_i by mixed additions -> partial.
+//   5. k_bucket_sum   one thread per bucket: sum of its chunk partials.
+//   6. bucket reduction sum_d d*B_d per window as a recursive running-sum: level l splits
+//                     its M inputs in segments of SEG, producing T_q = sum_t (t+off) V_t and
+//                     R_q = sum_t V_t; R becomes the next level's input (weight q), and
+//                     G_w = sum T0 + SEG*(sum T1 + SEG*(...)).  No scalar multiplications,
+//                     every thread chain is 2*SEG additions.
+//   7. k_tree_sum     per-window LDS tree sums of each level's T; k_window_horner folds the
+//                     levels; k_final folds the windows: sum_w 2^(c w) G_w.
+// Precompute factor F (bases table = F blocks of n bases, block f = 2^(c*Wg*f) * P) folds
+// the W windows into Wg = ceil(W/F) groups so the final fold shrinks to (Wg-1)*c doublings.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <vector>
+
+#include "mbls_common.hpp"
+#include "mbls_curve.hpp"
+
+namespace mbls {
+
+static constexpr uint32_t INVALID_KEY = 0xffffffffu;
+static constexpr int CHUNK = 16;  // max points per accumulation thread
+static constexpr int SEG = 16;    // inputs per reduction segment (power of two)
+static constexpr int SEG_LOG = 4;
+static constexpr int MAX_MSM_LOG = 26;
+static constexpr int SCAN_BLOCK = 1024;
+static constexpr int MAX_LEVELS = 8;
+
+struct MsmPlan {
+    int c, W, Wg, F;
+    uint32_t B, TB;
+    size_t contributions;
+    int levels;                 // bucket-reduction levels
+    uint32_t level_m[MAX_LEVELS];  // inputs per window at each level
+};
+
+eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p);
+
+// ---- non-templated launchers (msm_common.hip) ----------------------------------------
+eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* keys,
+                           uint32_t* vals, uint32_t* counts, hipStream_t st);
+eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint32_t* tmp, hipStream_t st);
+eIcicleError launch_chunk_counts(const uint32_t* counts, uint32_t* nchunks, uint32_t m, hipStream_t st);
+eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, size_t total, uint32_t* cursor,
+                            uint32_t* sorted, hipStream_t st);
+eIcicleError launch_chunk_owner(const uint32_t* chunk_off, uint32_t m, uint32_t* owner, hipStream_t st);
+eIcicleError launch_scalars_from_mont(uint8_t* s, size_t n, hipStream_t st);
+size_t scan_tmp_words(uint32_t m);
+
+// ------------------------------------------------------------------------------------
+// 4. accumulation: one thread per chunk of one bucket
+// ------------------------------------------------------------------------------------
+template <class F>
+__global__ __launch_bounds__(256) void k_accumulate(const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets,
+                                                    const uint32_t* __restrict__ chunk_off,
+                                                    const uint32_t* __restrict__ owner, uint32_t TB, uint32_t max_chunks,
+                                                    const uint8_t* __restrict__ bases, uint8_t* __restrict__ partials) {
+    uint32_t ch = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch >= max_chunks || ch >= chunk_off[TB]) return;
+    uint32_t b = owner[ch];
+    uint32_t k = ch - chunk_off[b];
+    uint32_t beg = offsets[b] + k * CHUNK;
+    uint32_t end = min(beg + CHUNK, offsets[b + 1]);
+    Jacobian<F> acc = Jacobian<F>::inf();
+    for (uint32_t e = beg; e < end; ++e) {
+        uint32_t v = sorted[e];
+        Affine<F> p = load_affine<F>(bases, v >> 1);
+        if (v & 1) p = aff_neg(p);
+        acc = jac_madd(acc, p);
+    }
+    store_jac<F>(partials, ch, acc);
+}
+
+// ------------------------------------------------------------------------------------
+// 5. bucket sums from chunk partials
+// ------------------------------------------------------------------------------------
+template <class F>
+__global__ __launch_bounds__(256) void k_bucket_sum(const uint32_t* __restrict__ chunk_off, uint32_t m,
+                                                    const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= m) return;
+    uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
+    Jacobian<F> acc = Jacobian<F>::inf();
+    if (k1 > k0) acc = load_jac<F>(partials, k0);
+    for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<F>(partials, k));
+    store_jac<F>(buckets, b, acc);
+}
+
+// ------------------------------------------------------------------------------------
+// 6. one level of the recursive running-sum reduction.
+//   in:  V[w * m_in + k], k < m_in, weight (k + off)
+//   out: T[w * m_out + q], R[w * m_out + q], m_out = ceil(m_in / SEG)
+// Single jac_add call site: the loop alternates the R and S updates.
+// ------------------------------------------------------------------------------------
+template <class F>
+__global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict__ V, uint32_t m_in, int Wg, int off,
+                                                      uint8_t* __restrict__ T, uint8_t* __restrict__ R) {
+    const uint32_t m_out = (m_in + SEG - 1) / SEG;
+    uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= m_out * (uint32_t)Wg) return;
+    const uint32_t w = tid / m_out, q = tid % m_out;
+    const uint32_t k0 = q * SEG;
+    const uint32_t k1 = min(k0 + SEG, m_in);  // exclusive
+    Jacobian<F> Racc = Jacobian<F>::inf(), Sacc = Jacobian<F>::inf();
+    // walk t = k1-1 .. k0: R += V_t; S += R unless (t - k0 + off) == 0
+    int steps = 2 * (int)(k1 - k0);
+    uint32_t t = k1 - 1;
+    for (int s = 0; s < steps; ++s) {
+        const bool r_step = (s & 1) == 0;
+        if (!r_step && (t - k0) + off == 0) {
+            if (t == k0) break;
+            --t;
+            continue;
+        }
+        Jacobian<F> x = r_step ? Racc : Sacc;
+        Jacobian<F> y = r_step ? load_jac<F>(V, (size_t)w * m_in + t) : Racc;
+        Jacobian<F> z = jac_add(x, y);
+        if (r_step) {
+            Racc = z;
+        } else {
+            Sacc = z;
+            if (t == k0) break;
+            --t;
+        }
+    }
+    store_jac<F>(T, tid, Sacc);
+    store_jac<F>(R, tid, Racc);
+}
+
+// per-window sum of `m` points: V[w * m + k] -> out[w]; one block per window
+template <class F>
+__global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V, uint32_t m, uint8_t* __restrict__ out,
+                                                  size_t out_stride_elems) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[64 * 3 * sizeof(F)];
+    const uint32_t w = blockIdx.x;
+    Jacobian<F> acc = Jacobian<F>::inf();
+    // 256 threads sweep sequentially, then waves fold via LDS (64 partials), then one wave
+    for (uint32_t k = threadIdx.x; k < m; k += 256) acc = jac_add(acc, load_jac<F>(V, (size_t)w * m + k));
+    // fold the 4 waves into 64 slots
+    for (int wave = 3; wave >= 0; --wave) {
+        if ((int)(threadIdx.x >> 6) == wave) {
+            if (wave < 3) acc = jac_add(acc, load_jac<F>(sh, threadIdx.x & 63));
+            store_jac<F>(sh, threadIdx.x & 63, acc);
+        }
+        __syncthreads();
+    }
+    for (int s = 32; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            acc = jac_add(acc, load_jac<F>(sh, threadIdx.x + s));
+            store_jac<F>(sh, threadIdx.x, acc);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) store_jac<F>(out, (size_t)w * out_stride_elems, acc);
+}
+
+// G_w = sumT[0] + SEG*(sumT[1] + SEG*(...)): sums laid out sums[l * Wg + w]
+template <class F>
+__global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, int Wg, uint8_t* __restrict__ windows) {
+    int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= Wg) return;
+    Jacobian<F> acc = load_jac<F>(sums, (size_t)(levels - 1) * Wg + w);
+    for (int l = levels - 2; l >= 0; --l) {
+        for (int k = 0; k < SEG_LOG; ++k) acc = jac_dbl(acc);
+        acc = jac_add(acc, load_jac<F>(sums, (size_t)l * Wg + w));
+    }
+    store_jac<F>(windows, w, acc);
+}
+
+// final fold over window groups: sum_w 2^(c w) G_w
+template <class F>
+__global__ void k_final(const uint8_t* __restrict__ windows, int Wg, int c, uint8_t* __restrict__ result) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    Jacobian<F> acc = load_jac<F>(windows, Wg - 1);
+    for (int w = Wg - 2; w >= 0; --w) {
+        for (int k = 0; k < c; ++k) acc = jac_dbl(acc);
+        acc = jac_add(acc, load_jac<F>(windows, w));
+    }
+    store_jac<F>(result, 0, acc);
+}
+
+template <class F>
+__global__ void k_store_inf(uint8_t* result, int count) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) store_jac<F>(result, i, Jacobian<F>::inf());
+}
+
+// ------------------------------------------------------------------------------------
+// conversions / utilities
+// ------------------------------------------------------------------------------------
+MBLS_DEV Fq to_mont_f(const Fq& a) { return to_mont(a); }
+MBLS_DEV Fq2 to_mont_f(const Fq2& a) { return {to_mont(a.c0), to_mont(a.c1)}; }
+MBLS_DEV Fq from_mont_f(const Fq& a) { return from_mont(a); }
+MBLS_DEV Fq2 from_mont_f(const Fq2& a) { return {from_mont(a.c0), from_mont(a.c1)}; }
+template <class F>
+MBLS_DEV F one_std();
+template <>
+MBLS_DEV Fq one_std<Fq>() {
+    Fq r = Fq::zero();
+    r.v[0] = 1;
+    return r;
+}
+template <>
+MBLS_DEV Fq2 one_std<Fq2>() {
+    Fq2 r = Fq2::zero();
+    r.c0.v[0] = 1;
+    return r;
+}
+
+template <class F>
+__global__ void k_points_to_mont(uint8_t* pts, size_t n) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Affine<F> p = load_affine<F>(pts, i);
+    p.x = to_mont_f(p.x);
+    p.y = to_mont_f(p.y);
+    store_affine<F>(pts, i, p);
+}
+
+// Jacobian Montgomery -> ICICLE standard projective (x, y, 1); identity (0, 1, 0)
+// (reference icicle_curve_api.cu:134-229)
+template <class F>
+__global__ void k_jac_to_icicle(uint8_t* pts, int count) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    Jacobian<F> p = load_jac<F>(pts, i);
+    Jacobian<F> o;
+    if (p.is_inf()) {
+        o.x = F::zero();
+        o.y = one_std<F>();
+        o.z = F::zero();
+    } else {
+        Affine<F> a = jac_to_affine(p);
+        o.x = from_mont_f(a.x);
+        o.y = from_mont_f(a.y);
+        o.z = one_std<F>();
+    }
+    store_jac<F>(pts, i, o);
+}
+
+template <class F>
+__global__ void k_sum_jac(const uint8_t* pts, int count, uint8_t* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    Jacobian<F> acc = Jacobian<F>::inf();
+    for (int i = 0; i < count; ++i) acc = jac_add(acc, load_jac<F>(pts, i));
+    store_jac<F>(out, 0, acc);
+}
+
+template <class F>
+MBLS_DEV Affine<F> generator();
+template <>
+MBLS_DEV Affine<Fq> generator<Fq>() { return g1_generator(); }
+template <>
+MBLS_DEV Affine<Fq2> generator<Fq2>() { return g2_generator(); }
+
+MBLS_DEV uint64_t splitmix64(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+
+// scalar i of stream `seed` (same as the oracle's gen_scalar): 4 splitmix64 words, masked to
+// 255 bits, minus r once if >= r
+MBLS_DEV Fr gen_scalar(uint64_t seed, uint64_t i) {
+    uint64_t base = splitmix64(seed) ^ (i * 0xd1342543de82ef95ULL);
+    Fr s;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint64_t l = splitmix64(base + (uint64_t)j * 0x632be59bd9b4e019ULL);
+        if (j == 3) l &= 0x7fffffffffffffffULL;
+        s.v[2 * j] = (uint32_t)l;
+        s.v[2 * j + 1] = (uint32_t)(l >> 32);
+    }
+    reduce_once(s);
+    return s;
+}
+
+// P_i = k_i * G (input generation only; not on the measured path)
+template <class F>
+__global__ void k_gen_bases(uint8_t* out, uint64_t seed, size_t n) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr k = gen_scalar(seed, i);
+    Jacobian<F> g = Jacobian<F>::from_affine(generator<F>());
+    store_affine<F>(out, i, jac_to_affine(jac_mul_u32(g, k.v)));
+}
+
+// precomputed bases: out[f*n + i] = 2^(shift*f) * P_i (Montgomery affine)
+template <class F>
+__global__ void k_precompute(const uint8_t* in, uint8_t* out, size_t n, int factor, int shift) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Affine<F> a = load_affine<F>(in, i);
+    store_affine<F>(out, i, a);
+    Jacobian<F> p = Jacobian<F>::from_affine(a);
+    for (int f = 1; f < factor; ++f) {
+        for (int k = 0; k < shift; ++k) p = jac_dbl(p);
+        store_affine<F>(out, (size_t)f * n + i, jac_to_affine(p));
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// host orchestration
+// ------------------------------------------------------------------------------------
+template <class F>
+struct GroupTraits;
+template <>
+struct GroupTraits<Fq> {
+    static constexpr size_t AFF = 96, JAC = 144;
+};
+template <>
+struct GroupTraits<Fq2> {
+    static constexpr size_t AFF = 192, JAC = 288;
+};
+
+struct MsmScratchSizes {
+    size_t keys, vals, sorted, words, tmp, owner, partials, buckets, levelT, levelR, sums, windows;
+    size_t total() const {
+        return keys + vals + sorted + 5 * words + tmp + owner + partials + buckets + levelT + levelR + sums + windows;
+    }
+};
+
+inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, uint32_t max_chunks) {
+    MsmScratchSizes z;
+    const size_t NC = P.contributions;
+    z.keys = align_up(NC * 4);
+    z.vals = align_up(NC * 4);
+    z.sorted = align_up(NC * 4);
+    z.words = align_up(((size_t)P.TB + 1) * 4);
+    z.tmp = align_up(scan_tmp_words(max_chunks > P.TB ? max_chunks : P.TB) * 4);
+    z.owner = align_up((size_t)max_chunks * 4);
+    z.partials = align_up((size_t)max_chunks * jac);
+    z.buckets = align_up((size_t)P.TB * jac);
+    size_t lv = 0;
+    for (int l = 0; l < P.levels; ++l) lv += (P.level_m[l] + SEG - 1) / SEG;
+    z.levelT = align_up(lv * P.Wg * jac);
+    z.levelR = align_up(lv * P.Wg * jac);
+    z.sums = align_up((size_t)P.levels * P.Wg * jac);
+    z.windows = align_up((size_t)P.Wg * jac);
+    return z;
+}
+
+// Core MSM on device operands: scalars (standard or Montgomery), bases Montgomery affine
+// (F*n entries when precomputed); result: one Jacobian Montgomery point on device.
+template <class F>
+eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t* bases, uint32_t n,
+                        const MsmPlan& P, uint8_t* result, Arena& arena, hipStream_t st) {
+    constexpr size_t JAC = GroupTraits<F>::JAC;
+    if (n == 0) {
+        hipLaunchKernelGGL(k_store_inf<F>, dim3(1), dim3(64), 0, st, result, 1);
+        MBLS_TRY(hipGetLastError());
+        return MBLS_SUCCESS;
+    }
+    const uint32_t TB = P.TB;
+    const size_t NC = P.contributions;
+    const uint32_t max_chunks = (uint32_t)(NC / CHUNK + TB + 1);
+    MsmScratchSizes z = msm_scratch_sizes(P, JAC, max_chunks);
+    uint32_t* keys = (uint32_t*)arena.take(z.keys);
+    uint32_t* vals = (uint32_t*)arena.take(z.vals);
+    uint32_t* sorted = (uint32_t*)arena.take(z.sorted);
+    uint32_t* counts = (uint32_t*)arena.take(z.words);
+    uint32_t* offsets = (uint32_t*)arena.take(z.words);
+    uint32_t* cursor = (uint32_t*)arena.take(z.words);
+    uint32_t* nchunks = (uint32_t*)arena.take(z.words);
+    uint32_t* chunk_off = (uint32_t*)arena.take(z.words);
+    uint32_t* tmp = (uint32_t*)arena.take(z.tmp);
+    uint32_t* owner = (uint32_t*)arena.take(z.owner);
+    uint8_t* partials = (uint8_t*)arena.take(z.partials);
+    uint8_t* buckets = (uint8_t*)arena.take(z.buckets);
+    uint8_t* levelT = (uint8_t*)arena.take(z.levelT);
+    uint8_t* levelR = (uint8_t*)arena.take(z.levelR);
+    uint8_t* sums = (uint8_t*)arena.take(z.sums);
+    uint8_t* windows = (uint8_t*)arena.take(z.windows);
+    if (!windows) return MBLS_ALLOCATION_FAILED;
+
+    MBLS_TRY(hipMemsetAsync(counts, 0, (size_t)TB * 4, st));
+    eIcicleError er = launch_digits(scalars, scalars_mont, n, P, keys, vals, counts, st);
+    if (er != MBLS_SUCCESS) return er;
+    if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) return er;
+    MBLS_TRY(hipMemcpyAsync(cursor, offsets, (size_t)TB * 4, hipMemcpyDeviceToDevice, st));
+    if ((er = launch_chunk_counts(counts, nchunks, TB, st)) != MBLS_SUCCESS) return er;
+    if ((er = scan_exclusive(nchunks, chunk_off, TB, tmp, st)) != MBLS_SUCCESS) return er;
+    if ((er = launch_scatter(keys, vals, NC, cursor, sorted, st)) != MBLS_SUCCESS) return er;
+    if ((er = launch_chunk_owner(chunk_off, TB, owner, st)) != MBLS_SUCCESS) return er;
+    // the chunk count is data dependent: launch the bound, extra threads exit
+    hipLaunchKernelGGL(k_accumulate<F>, dim3((max_chunks + 255) / 256), dim3(256), 0, st, sorted, offsets, chunk_off,
+                       owner, TB, max_chunks, bases, partials);
+    hipLaunchKernelGGL(k_bucket_sum<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials, buckets);
+    // recursive running-sum reduction
+    const uint8_t* V = buckets;
+    size_t lvoff = 0;
+    for (int l = 0; l < P.levels; ++l) {
+        uint32_t m_in = P.level_m[l];
+        uint32_t m_out = (m_in + SEG - 1) / SEG;
+        uint8_t* T = levelT + lvoff * JAC;
+        uint8_t* R = levelR + lvoff * JAC;
+        uint32_t threads = m_out * (uint32_t)P.Wg;
+        hipLaunchKernelGGL(k_reduce_level<F>, dim3((threads + 255) / 256), dim3(256), 0, st, V, m_in, P.Wg,
+                           l == 0 ? 1 : 0, T, R);
+        hipLaunchKernelGGL(k_tree_sum<F>, dim3(P.Wg), dim3(256), 0, st, T, m_out, sums + (size_t)l * P.Wg * JAC,
+                           (size_t)1);
+        V = R;
+        lvoff += (size_t)m_out * P.Wg;
+    }
+    hipLaunchKernelGGL(k_window_horner<F>, dim3((P.Wg + 63) / 64), dim3(64), 0, st, sums, P.levels, P.Wg, windows);
+    hipLaunchKernelGGL(k_final<F>, dim3(1), dim3(64), 0, st, windows, P.Wg, P.c, result);
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
+}
+
+// ------------------------------------------------------------------------------------
+// boundary wrappers (placement flags, Montgomery flags, batch, ICICLE result format)
+// ------------------------------------------------------------------------------------
+template <class F>
+eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, const MSMConfig* cfg, void* results,
+                      bool icicle_semantics) {
+    constexpr size_t AFF = GroupTraits<F>::AFF, JAC = GroupTraits<F>::JAC;
+    if (!cfg || !results) return MBLS_INVALID_POINTER;
+    if (msm_size < 0 || msm_size > (1 << MAX_MSM_LOG)) return MBLS_INVALID_ARGUMENT;
+    if (msm_size > 0 && (!scalars || !bases)) return MBLS_INVALID_POINTER;
+    hipStream_t st = static_cast<hipStream_t>(cfg->stream);
+    const int batch = icicle_semantics ? (cfg->batch_size > 0 ? cfg->batch_size : 1) : 1;
+    MsmPlan P;
+    eIcicleError er = make_plan(msm_size > 0 ? msm_size : 1, cfg, P);
+    if (er != MBLS_SUCCESS) return er;
+    const bool scal_mont = icicle_semantics ? cfg->are_scalars_montgomery_form : false;
+    const bool pts_mont = icicle_semantics ? cfg->are_points_montgomery_form : true;
+    const bool shared = cfg->are_points_shared_in_batch || batch == 1;
+    const size_t n = (size_t)msm_size;
+    const size_t nbases_per = n * (size_t)P.F;
+    const size_t nbases = shared ? nbases_per : nbases_per * batch;
+
+    StreamCtx& ctx = stream_ctx(st);
+    std::lock_guard<std::mutex> lk(ctx.mu);
+    Arena& A = ctx.arena;
+    A.reset();
+    size_t st_s = (!cfg->are_scalars_on_device) ? align_up(n * 32 * batch) : 0;
+    size_t st_b = (!cfg->are_points_on_device || !pts_mont) ? align_up(nbases * AFF) : 0;
+    size_t st_r = align_up(JAC * (size_t)batch);
+    uint32_t max_chunks = (uint32_t)(P.contributions / CHUNK + P.TB + 1);
+    size_t scratch = msm_scratch_sizes(P, JAC, max_chunks).total();
+    er = A.reserve(st_s + st_b + st_r + scratch + 4096);
+    if (er != MBLS_SUCCESS) return er;
+
+    const uint8_t* d_s = static_cast<const uint8_t*>(scalars);
+    const uint8_t* d_b = static_cast<const uint8_t*>(bases);
+    if (st_s) {
+        void* t = A.take(n * 32 * batch);
+        MBLS_TRY(hipMemcpyAsync(t, scalars, n * 32 * batch, hipMemcpyHostToDevice, st));
+        d_s = static_cast<const uint8_t*>(t);
+    }
+    if (st_b) {
+        void* t = A.take(nbases * AFF);
+        MBLS_TRY(hipMemcpyAsync(t, bases, nbases * AFF,
+                                cfg->are_points_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+        if (!pts_mont) {
+            hipLaunchKernelGGL(k_points_to_mont<F>, dim3((unsigned)((nbases + 255) / 256)), dim3(256), 0, st,
+                               (uint8_t*)t, nbases);
+            MBLS_TRY(hipGetLastError());
+        }
+        d_b = static_cast<const uint8_t*>(t);
+    }
+    uint8_t* d_r = static_cast<uint8_t*>(A.take(JAC * (size_t)batch));
+    const size_t mark = A.mark();
+    for (int b = 0; b < batch; ++b) {
+        A.rewind(mark);  // scratch reused across the batch (stream-ordered)
+        const uint8_t* sb = d_s + (size_t)b * n * 32;
+        const uint8_t* bb = d_b + (shared ? 0 : (size_t)b * nbases_per * AFF);
+        er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, A, st);
+        if (er != MBLS_SUCCESS) return er;
+    }
+    if (icicle_semantics) {
+        hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch + 63) / 64), dim3(64), 0, st, d_r, batch);
+        MBLS_TRY(hipGetLastError());
+    }
+    MBLS_TRY(hipMemcpyAsync(results, d_r, JAC * (size_t)batch,
+                            cfg->are_results_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
+    if (!cfg->is_async || !cfg->are_results_on_device || st_s || (st_b && !cfg->are_points_on_device))
+        MBLS_TRY(hipStreamSynchronize(st));
+    return MBLS_SUCCESS;
+}
+
+template <class F>
+eIcicleError precompute_call(const void* in, int n, const MSMConfig* cfg, void* out) {
+    constexpr size_t AFF = GroupTraits<F>::AFF;
+    if (!cfg || !in || !out) return MBLS_INVALID_POINTER;
+    if (n < 0) return MBLS_INVALID_ARGUMENT;
+    int factor = cfg->precompute_factor > 0 ? cfg->precompute_factor : 1;
+    MsmPlan P;
+    eIcicleError er = make_plan(n > 0 ? n : 1, cfg, P);
+    if (er != MBLS_SUCCESS) return er;
+    if (factor > P.W) return MBLS_INVALID_ARGUMENT;
+    if (!cfg->are_points_montgomery_form) return MBLS_API_NOT_IMPLEMENTED;
+    if (n == 0) return MBLS_SUCCESS;
+    hipStream_t st = static_cast<hipStream_t>(cfg->stream);
+    StreamCtx& ctx = stream_ctx(st);
+    std::lock_guard<std::mutex> lk(ctx.mu);
+    Arena& A = ctx.arena;
+    A.reset();
+    size_t in_b = (size_t)n * AFF, out_b = in_b * factor;
+    er = A.reserve(align_up(in_b) + align_up(out_b));
+    if (er != MBLS_SUCCESS) return er;
+    uint8_t* din = (uint8_t*)A.take(in_b);
+    uint8_t* dout = (uint8_t*)A.take(out_b);
+    MBLS_TRY(hipMemcpyAsync(din, in, in_b, cfg->are_points_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_precompute<F>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, st, din, dout, (size_t)n, factor,
+                       P.c * P.Wg);
+    MBLS_TRY(hipGetLastError());
+    MBLS_TRY(hipMemcpyAsync(out, dout, out_b, cfg->are_results_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
+    MBLS_TRY(hipStreamSynchronize(st));
+    return MBLS_SUCCESS;
+}
+
+}  // namespace mbls

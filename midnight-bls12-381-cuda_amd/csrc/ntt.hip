@@ -1,0 +1,502 @@
+// ntt.hip -- radix-2 Fr NTT for CDNA4, natural order in and out.
+//
+// Semantics = the CPU path the prover uses (core/ntt.rs:1488-1603, midnight_curves best_fft):
+//   forward  X_j = sum_i x_i w^(ij),  inverse  x_i = n^-1 sum_j X_j w^(-ij),
+//   w = ROOT_OF_UNITY^(2^(32-k)) for n = 2^k, ROOT_OF_UNITY = 7^((r-1)/2^32).
+// The reference GPU NTT (ntt_kernels.cu:710-958) derives its twiddles from whatever root the
+// caller passes assuming order 2^24 (ntt_kernels.cu:1614,1644) and does not match best_fft
+// (SURVEY.md finding 2); we do not reproduce that.
+//
+// Data layout in HBM: n contiguous 32-byte Fr values per polynomial, batch polynomials
+// back to back (columns_batch = false).  Twiddle table: w_K^i, i < 2^(K-1), Montgomery, plus
+// the inverse table, K = the domain's max log size (twiddle of stage m = 2^s, index j is
+// table[j * 2^(K-s)]).
+//
+// Kernel structure: ceil(k / 10) passes, each a LDS-resident tile of T = 1024 elements
+// (32 KiB) doing up to 10 radix-2 DIT stages between __syncthreads.  Pass 1 fuses the
+// bit-reversal permutation into its gather: it reads C adjacent columns of the input viewed
+// as a 2^L x 2^(k-L) matrix (coalesced C*32-byte rows) and writes contiguous DIT blocks.
+// Later passes read/write tiles of 2^L strided rows x C adjacent columns in place.  The
+// inverse's n^-1 scaling is fused into the last pass's store.
+// Algorithmic traffic: 64 B per element per transform (one read + one write of 32 B);
+// actual traffic = passes * 64 B + twiddle reads.  Arithmetic: (n/2) log n Montgomery
+// products -- the kernel is VALU-bound on gfx950.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <mutex>
+
+#include "mbls_common.hpp"
+#include "mbls_field.hpp"
+
+namespace mbls {
+
+static constexpr int NTT_TILE_LOG = 10;
+static constexpr int NTT_TILE = 1 << NTT_TILE_LOG;  // elements per workgroup tile
+static constexpr int NTT_THREADS = 256;
+
+// canonical 2^32-th root of unity, Montgomery (bls12_381_constants.h:127-130)
+static const uint64_t ROOT_2_32_MONT[4] = {0xb9b58d8c5f0e466aULL, 0x5b1b4c801819d7ecULL, 0x0af53ae352a31e64ULL,
+                                           0x5bf3adda19e9b27bULL};
+
+struct Domain {
+    int max_log = 0;
+    uint8_t* tw = nullptr;      // w^i, i < 2^(max_log-1)
+    uint8_t* tw_inv = nullptr;  // w^-i
+};
+
+static std::mutex g_domain_mu;
+static Domain g_domain;
+
+__device__ __forceinline__ uint32_t bitrev(uint32_t x, int bits) {
+    return bits == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - bits));
+}
+
+// table[i] = w^i for i < count (one exponentiation per entry: init only)
+__global__ void k_twiddles(uint8_t* table, Fr w, uint32_t count) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    Fr acc = Fr::one();
+    Fr b = w;
+    uint32_t e = i;
+    while (e) {
+        if (e & 1) acc = acc * b;
+        b = sqr(b);
+        e >>= 1;
+    }
+    store<FrCfg>(table + 32 * (size_t)i, acc);
+}
+
+// One pass of up to NTT_TILE_LOG DIT stages.
+//   FIRST: stages 1..L with the bit-reversal gather from `in`; else stages s0+1..s0+L in place.
+//   SCALE: multiply outputs by `scale` (inverse n^-1) on store.
+template <bool FIRST, bool SCALE>
+__global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ out, const uint8_t* __restrict__ in,
+                                                          const uint8_t* __restrict__ tw, int log_n, int s0, int L,
+                                                          int logC, int tw_log, Fr scale) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[NTT_TILE * 32];
+    const int C = 1 << logC;
+    const int rows = 1 << L;
+    const int T = rows * C;  // active tile elements (== NTT_TILE except for tiny transforms)
+    const size_t n = (size_t)1 << log_n;
+    const int tiles_per_poly = (int)(n >> (L + logC));
+    const int poly = blockIdx.x / tiles_per_poly;
+    const int tile = blockIdx.x % tiles_per_poly;
+    const size_t pbase = (size_t)poly * n;
+
+    // ---- load tile into LDS as [row t][col c]
+    if (FIRST) {
+        // input viewed as 2^L rows x 2^(k-L) cols; tile = cols [c0, c0 + C)
+        const int colbits = log_n - L;
+        const size_t c0 = (size_t)tile * C;
+        for (int e = threadIdx.x; e < T; e += NTT_THREADS) {
+            int c = e & (C - 1), tr = e >> logC;  // source row tr
+            size_t src = pbase + ((size_t)tr << colbits) + c0 + c;
+            Fr v = load<FrCfg>(in + 32 * src);
+            int p = (int)bitrev((uint32_t)tr, L);  // DIT position inside the block
+            store<FrCfg>(lds + 32 * (p * C + c), v);
+        }
+    } else {
+        // rows t: stride 2^s0; cols lo in [lo0, lo0 + C) inside the low 2^s0 block
+        const int lo_tiles = (int)(((size_t)1 << s0) >> logC);
+        const size_t hi = tile / lo_tiles;
+        const size_t lo0 = (size_t)(tile % lo_tiles) * C;
+        for (int e = threadIdx.x; e < T; e += NTT_THREADS) {
+            int c = e & (C - 1), t = e >> logC;
+            size_t idx = pbase + (hi << (s0 + L)) + ((size_t)t << s0) + lo0 + c;
+            Fr v = load<FrCfg>(out + 32 * idx);
+            store<FrCfg>(lds + 32 * e, v);
+        }
+    }
+    __syncthreads();
+
+    // ---- L radix-2 DIT stages
+    const size_t lo_base = FIRST ? 0 : (size_t)(tile % (int)(((size_t)1 << s0) >> logC)) * C;
+    for (int l = 1; l <= L; ++l) {
+        const int half = 1 << (l - 1);
+        const int s = s0 + l;  // global stage, m = 2^s
+        for (int u = threadIdx.x; u < T / 2; u += NTT_THREADS) {
+            int c = u & (C - 1);
+            int r = u >> logC;
+            int g = r >> (l - 1);
+            int j = r & (half - 1);
+            int t0 = (g << l) + j;
+            int t1 = t0 + half;
+            Fr a = load<FrCfg>(lds + 32 * (t0 * C + c));
+            Fr b = load<FrCfg>(lds + 32 * (t1 * C + c));
+            if (l > 1 || !FIRST) {
+                size_t jj = ((size_t)j << s0) + (FIRST ? 0 : lo_base + c);
+                Fr w = load<FrCfg>(tw + 32 * (jj << (tw_log - s)));
+                b = b * w;
+            }
+            store<FrCfg>(lds + 32 * (t0 * C + c), a + b);
+            store<FrCfg>(lds + 32 * (t1 * C + c), a - b);
+        }
+        __syncthreads();
+    }
+
+    // ---- store
+    if (FIRST) {
+        const int colbits = log_n - L;
+        const size_t c0 = (size_t)tile * C;
+        for (int e = threadIdx.x; e < T; e += NTT_THREADS) {
+            // write block by block: consecutive threads -> consecutive positions of one block
+            int p = e & (rows - 1), c = e >> L;
+            size_t blk = bitrev((uint32_t)(c0 + c), colbits);
+            Fr v = load<FrCfg>(lds + 32 * (p * C + c));
+            if (SCALE) v = v * scale;
+            store<FrCfg>(out + 32 * (pbase + (blk << L) + p), v);
+        }
+    } else {
+        const int lo_tiles = (int)(((size_t)1 << s0) >> logC);
+        const size_t hi = tile / lo_tiles;
+        const size_t lo0 = (size_t)(tile % lo_tiles) * C;
+        for (int e = threadIdx.x; e < T; e += NTT_THREADS) {
+            int c = e & (C - 1), t = e >> logC;
+            Fr v = load<FrCfg>(lds + 32 * e);
+            if (SCALE) v = v * scale;
+            store<FrCfg>(out + 32 * (pbase + (hi << (s0 + L)) + ((size_t)t << s0) + lo0 + c), v);
+        }
+    }
+}
+
+__global__ void k_copy_scale(uint8_t* out, const uint8_t* in, size_t count, Fr scale, int do_scale) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    Fr v = load<FrCfg>(in + 32 * i);
+    if (do_scale) v = v * scale;
+    store<FrCfg>(out + 32 * i, v);
+}
+
+// ---- host-side field helpers (tiny, init-time only) ----------------------------------
+typedef unsigned __int128 u128;
+static const uint64_t HFR_P[4] = {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL,
+                                  0x73eda753299d7d48ULL};
+static const uint64_t HFR_ONE[4] = {0x00000001fffffffeULL, 0x5884b7fa00034802ULL, 0x998c4fefecbc4ff5ULL,
+                                    0x1824b159acc5056fULL};
+static const uint64_t HFR_R2[4] = {0xc999e990f3f29c6dULL, 0x2b6cedcb87925c23ULL, 0x05d314967254398fULL,
+                                   0x0748d9d99f59ff11ULL};
+
+static void hfr_mul(uint64_t* r, const uint64_t* a, const uint64_t* b) {
+    uint64_t t[6] = {0};
+    for (int i = 0; i < 4; ++i) {
+        uint64_t c = 0;
+        for (int j = 0; j < 4; ++j) {
+            u128 s = (u128)a[j] * b[i] + t[j] + c;
+            t[j] = (uint64_t)s;
+            c = (uint64_t)(s >> 64);
+        }
+        u128 s = (u128)t[4] + c;
+        t[4] = (uint64_t)s;
+        t[5] = (uint64_t)(s >> 64);
+        uint64_t q = t[0] * 0xfffffffeffffffffULL;
+        s = (u128)q * HFR_P[0] + t[0];
+        c = (uint64_t)(s >> 64);
+        for (int j = 1; j < 4; ++j) {
+            s = (u128)q * HFR_P[j] + t[j] + c;
+            t[j - 1] = (uint64_t)s;
+            c = (uint64_t)(s >> 64);
+        }
+        s = (u128)t[4] + c;
+        t[3] = (uint64_t)s;
+        t[4] = t[5] + (uint64_t)(s >> 64);
+    }
+    bool ge = t[4] != 0;
+    if (!ge) {
+        ge = true;
+        for (int i = 3; i >= 0; --i)
+            if (t[i] != HFR_P[i]) {
+                ge = t[i] > HFR_P[i];
+                break;
+            }
+    }
+    if (ge) {
+        uint64_t br = 0;
+        for (int i = 0; i < 4; ++i) {
+            u128 d = (u128)t[i] - HFR_P[i] - br;
+            t[i] = (uint64_t)d;
+            br = (uint64_t)(d >> 64) & 1;
+        }
+    }
+    memcpy(r, t, 32);
+}
+
+static bool hfr_eq(const uint64_t* a, const uint64_t* b) { return memcmp(a, b, 32) == 0; }
+
+static void hfr_pow(uint64_t* r, const uint64_t* a, const uint64_t* e) {
+    uint64_t acc[4];
+    memcpy(acc, HFR_ONE, 32);
+    for (int i = 255; i >= 0; --i) {
+        hfr_mul(acc, acc, acc);
+        if ((e[i / 64] >> (i % 64)) & 1) hfr_mul(acc, acc, a);
+    }
+    memcpy(r, acc, 32);
+}
+
+static void hfr_inv(uint64_t* r, const uint64_t* a) {
+    uint64_t e[4];
+    memcpy(e, HFR_P, 32);
+    e[0] -= 2;
+    hfr_pow(r, a, e);
+}
+
+// order of `w` (Montgomery) as a power of two, or -1
+static int hfr_log_order(const uint64_t* w) {
+    uint64_t x[4];
+    memcpy(x, w, 32);
+    for (int k = 0; k <= 32; ++k) {
+        if (hfr_eq(x, HFR_ONE)) return k;
+        hfr_mul(x, x, x);
+    }
+    return -1;
+}
+
+static void canonical_omega(uint64_t* w, int log_n) {
+    memcpy(w, ROOT_2_32_MONT, 32);
+    for (int k = log_n; k < 32; ++k) hfr_mul(w, w, w);
+}
+
+static Fr to_dev(const uint64_t* h) {
+    Fr r;
+    memcpy(r.v, h, 32);
+    return r;
+}
+
+static eIcicleError build_domain(int max_log, hipStream_t st) {
+    if (g_domain.max_log >= max_log && g_domain.tw) return MBLS_SUCCESS;
+    if (g_domain.tw) {
+        MBLS_TRY(hipDeviceSynchronize());
+        (void)hipFree(g_domain.tw);
+        (void)hipFree(g_domain.tw_inv);
+        g_domain = Domain{};
+    }
+    size_t count = max_log > 0 ? ((size_t)1 << (max_log - 1)) : 1;
+    uint8_t *tw = nullptr, *twi = nullptr;
+    MBLS_TRY(hipMalloc(&tw, 32 * count));
+    hipError_t e2 = hipMalloc(&twi, 32 * count);
+    if (e2 != hipSuccess) {
+        (void)hipFree(tw);
+        return map_hip_error(e2, "ntt twiddle alloc");
+    }
+    uint64_t w[4], wi[4];
+    canonical_omega(w, max_log);
+    hfr_inv(wi, w);
+    int blocks = (int)((count + 255) / 256);
+    hipLaunchKernelGGL(k_twiddles, dim3(blocks), dim3(256), 0, st, tw, to_dev(w), (uint32_t)count);
+    hipLaunchKernelGGL(k_twiddles, dim3(blocks), dim3(256), 0, st, twi, to_dev(wi), (uint32_t)count);
+    MBLS_TRY(hipGetLastError());
+    MBLS_TRY(hipStreamSynchronize(st));
+    g_domain.max_log = max_log;
+    g_domain.tw = tw;
+    g_domain.tw_inv = twi;
+    return MBLS_SUCCESS;
+}
+
+// enqueue forward/inverse NTT of `batch` polynomials of 2^log_n on device buffers
+eIcicleError ntt_device(uint8_t* out, const uint8_t* in, int log_n, bool inverse, int batch, hipStream_t st) {
+    const Domain& D = g_domain;
+    if (!D.tw || log_n > D.max_log) return MBLS_INVALID_ARGUMENT;
+    const size_t n = (size_t)1 << log_n;
+    const uint8_t* tw = inverse ? D.tw_inv : D.tw;
+    uint64_t ninv_h[4] = {0, 0, 0, 0};
+    if (inverse) {
+        uint64_t nm[4] = {n, 0, 0, 0};
+        hfr_mul(nm, nm, HFR_R2);  // n in Montgomery form
+        hfr_inv(ninv_h, nm);
+    }
+    Fr scale = to_dev(inverse ? ninv_h : HFR_ONE);
+    if (log_n == 0) {
+        size_t cnt = (size_t)batch;
+        hipLaunchKernelGGL(k_copy_scale, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, out, in, cnt, scale, 0);
+        MBLS_TRY(hipGetLastError());
+        return MBLS_SUCCESS;
+    }
+    // split the k stages into passes of <= NTT_TILE_LOG stages
+    int npass = (log_n + NTT_TILE_LOG - 1) / NTT_TILE_LOG;
+    int s0 = 0;
+    for (int p = 0; p < npass; ++p) {
+        int remaining = log_n - s0;
+        int L = (remaining + (npass - p) - 1) / (npass - p);
+        bool first = (p == 0);
+        bool last = (p == npass - 1);
+        // columns per tile: limited by the tile size and by the available column count
+        int colspace = first ? (log_n - L) : s0;
+        int logC = NTT_TILE_LOG - L;
+        if (logC > colspace) logC = colspace;
+        size_t tiles = (n >> (L + logC)) * (size_t)batch;
+        if (tiles > 0x7fffffff) return MBLS_INVALID_ARGUMENT;
+        dim3 grid((unsigned)tiles), blk(NTT_THREADS);
+        if (first && last && inverse)
+            hipLaunchKernelGGL((k_ntt_pass<true, true>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, D.max_log, scale);
+        else if (first)
+            hipLaunchKernelGGL((k_ntt_pass<true, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, D.max_log, scale);
+        else if (last && inverse)
+            hipLaunchKernelGGL((k_ntt_pass<false, true>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, D.max_log, scale);
+        else
+            hipLaunchKernelGGL((k_ntt_pass<false, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, D.max_log, scale);
+        MBLS_TRY(hipGetLastError());
+        s0 += L;
+    }
+    return MBLS_SUCCESS;
+}
+
+static int log2_exact(long long n) {
+    if (n <= 0 || (n & (n - 1))) return -1;
+    int k = 0;
+    while ((1LL << k) < n) ++k;
+    return k;
+}
+
+eIcicleError ntt_init_domain(const mbls_fr_t* root, const NTTInitDomainConfig* cfg) {
+    if (!root) return MBLS_INVALID_POINTER;
+    hipStream_t st = cfg ? static_cast<hipStream_t>(cfg->stream) : nullptr;
+    // The root only sizes the domain: its order 2^K (read as Montgomery, else as standard
+    // form).  Twiddles are always the canonical best_fft roots (see file header).
+    int K = hfr_log_order(root->limbs);
+    if (K < 0) {
+        uint64_t m[4];
+        hfr_mul(m, root->limbs, HFR_R2);
+        K = hfr_log_order(m);
+    }
+    if (K < 0) return MBLS_INVALID_ARGUMENT;
+    if (K > 27) K = 27;  // 2^27 Fr twiddles = 4 GiB per table: cap the eager tables
+    std::lock_guard<std::mutex> lk(g_domain_mu);
+    return build_domain(K, st);
+}
+
+eIcicleError ntt_release_domain() {
+    std::lock_guard<std::mutex> lk(g_domain_mu);
+    if (g_domain.tw) {
+        MBLS_TRY(hipDeviceSynchronize());
+        (void)hipFree(g_domain.tw);
+        (void)hipFree(g_domain.tw_inv);
+    }
+    g_domain = Domain{};
+    return MBLS_SUCCESS;
+}
+
+// coset scaling x_i *= g^(+-i) within each polynomial (device, in place)
+__global__ void k_coset_scale(uint8_t* data, Fr g, size_t n, size_t total) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    size_t e = i & (n - 1);
+    Fr acc = Fr::one(), b = g;
+    while (e) {
+        if (e & 1) acc = acc * b;
+        b = sqr(b);
+        e >>= 1;
+    }
+    Fr v = load<FrCfg>(data + 32 * i);
+    store<FrCfg>(data + 32 * i, v * acc);
+}
+
+// Full ICICLE-semantics NTT call: staging, batch, coset; natural ordering only.
+eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTConfig* cfg, mbls_fr_t* output,
+                      const mbls_fr_t* coset_gen) {
+    if (!input || !output || !cfg) return MBLS_INVALID_POINTER;
+    int log_n = log2_exact(size);
+    if (log_n < 0) return MBLS_INVALID_ARGUMENT;
+    if (cfg->ordering != MBLS_ORDERING_NN) return MBLS_API_NOT_IMPLEMENTED;
+    if (cfg->columns_batch) return MBLS_API_NOT_IMPLEMENTED;
+    int batch = cfg->batch_size > 0 ? cfg->batch_size : 1;
+    hipStream_t st = static_cast<hipStream_t>(cfg->stream);
+    {
+        std::lock_guard<std::mutex> lk(g_domain_mu);
+        if (!g_domain.tw || g_domain.max_log < log_n) {
+            // lazily size the domain (the Rust side initialises once with its max size)
+            eIcicleError er = build_domain(log_n < 20 ? 20 : log_n, st);
+            if (er != MBLS_SUCCESS) return er;
+        }
+    }
+    const size_t bytes = (size_t)size * 32 * (size_t)batch;
+    StreamCtx& ctx = stream_ctx(st);
+    std::lock_guard<std::mutex> lk(ctx.mu);
+    size_t need = 0;
+    if (!cfg->are_inputs_on_device) need += align_up(bytes);
+    if (!cfg->are_outputs_on_device) need += align_up(bytes);
+    ctx.arena.reset();
+    eIcicleError er = ctx.arena.reserve(need);
+    if (er != MBLS_SUCCESS) return er;
+    const uint8_t* din = reinterpret_cast<const uint8_t*>(input);
+    uint8_t* dout = reinterpret_cast<uint8_t*>(output);
+    if (!cfg->are_inputs_on_device) {
+        void* t = ctx.arena.take(bytes);
+        MBLS_TRY(hipMemcpyAsync(t, input, bytes, hipMemcpyHostToDevice, st));
+        din = static_cast<const uint8_t*>(t);
+    }
+    if (!cfg->are_outputs_on_device) dout = static_cast<uint8_t*>(ctx.arena.take(bytes));
+
+    // coset: forward evaluates on g*H (pre-scale by g^i); inverse post-scales by g^-i
+    bool coset = false;
+    uint64_t g[4];
+    if (coset_gen) {
+        memcpy(g, coset_gen->limbs, 32);
+        coset = !hfr_eq(g, HFR_ONE);
+    }
+    const size_t total = (size_t)size * batch;
+    const bool inverse = (dir == MBLS_NTT_INVERSE);
+    if (coset && !inverse) {
+        if (din != dout) MBLS_TRY(hipMemcpyAsync(dout, din, bytes, hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(k_coset_scale, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dout, to_dev(g),
+                           (size_t)size, total);
+        MBLS_TRY(hipGetLastError());
+        din = dout;
+    }
+    if (din == dout && log_n > 0) {
+        // the first pass gathers bit-reversed: needs a distinct source
+        void* t = nullptr;
+        // in-place request: copy the input aside (arena grows once; keeps earlier pointers
+        // valid because growth only happens before any take in this call)
+        ctx.arena.reset();
+        size_t need2 = need + align_up(bytes);
+        er = ctx.arena.reserve(need2);
+        if (er != MBLS_SUCCESS) return er;
+        // re-take in the same order so previous pointers stay identical
+        if (!cfg->are_inputs_on_device) ctx.arena.take(bytes);
+        if (!cfg->are_outputs_on_device) ctx.arena.take(bytes);
+        t = ctx.arena.take(bytes);
+        MBLS_TRY(hipMemcpyAsync(t, din, bytes, hipMemcpyDeviceToDevice, st));
+        din = static_cast<const uint8_t*>(t);
+    }
+    er = ntt_device(dout, din, log_n, inverse, batch, st);
+    if (er != MBLS_SUCCESS) return er;
+    if (coset && inverse) {
+        uint64_t gi[4];
+        hfr_inv(gi, g);
+        hipLaunchKernelGGL(k_coset_scale, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dout, to_dev(gi),
+                           (size_t)size, total);
+        MBLS_TRY(hipGetLastError());
+    }
+    if (!cfg->are_outputs_on_device) MBLS_TRY(hipMemcpyAsync(output, dout, bytes, hipMemcpyDeviceToHost, st));
+    if (!cfg->is_async || !cfg->are_outputs_on_device || !cfg->are_inputs_on_device) MBLS_TRY(hipStreamSynchronize(st));
+    return MBLS_SUCCESS;
+}
+
+}  // namespace mbls
+
+using namespace mbls;
+
+extern "C" {
+
+eIcicleError bls12_381_ntt_init_domain_cuda(const mbls_fr_t* root_of_unity, const NTTInitDomainConfig* config) {
+    return ntt_init_domain(root_of_unity, config);
+}
+eIcicleError bls12_381_ntt_release_domain_cuda(void) { return ntt_release_domain(); }
+eIcicleError bls12_381_ntt_cuda(const mbls_fr_t* input, int size, NTTDir dir, const NTTConfig* config,
+                                mbls_fr_t* output) {
+    return ntt_call(input, size, dir, config, output, config ? &config->coset_gen : nullptr);
+}
+eIcicleError bls12_381_coset_ntt_cuda(const mbls_fr_t* input, int size, NTTDir dir, const mbls_fr_t* coset_gen,
+                                      const NTTConfig* config, mbls_fr_t* output) {
+    return ntt_call(input, size, dir, config, output, coset_gen);
+}
+eIcicleError bls12_381_field_ntt_cuda(const mbls_fr_t* input, int size, NTTDir dir, const NTTConfig* config,
+                                      mbls_fr_t* output) {
+    return ntt_call(input, size, dir, config, output, config ? &config->coset_gen : nullptr);
+}
+eIcicleError bls12_381_field_ntt_init_domain_cuda(const mbls_fr_t* root_of_unity, const NTTInitDomainConfig* config) {
+    return ntt_init_domain(root_of_unity, config);
+}
+eIcicleError bls12_381_field_ntt_release_domain_cuda(void) { return ntt_release_domain(); }
+
+}  // extern "C"

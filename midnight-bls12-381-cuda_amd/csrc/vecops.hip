@@ -1,0 +1,189 @@
+// vecops.hip -- element-wise Fr vector operations (HBM-streaming kernels).
+//
+// Reference: kernels bls12-381/src/field/vec_ops.cu:63-118,335-345, boundary wrappers
+// icicle_field_api.cu:133-334 (run_vec_op, scalar_*_vec_cuda_impl) and the exported C entry
+// points vec_ops.cu:393-476 (vec_*_cuda) and :693-840 (bls12_381_vector_*).
+//
+// Algorithmic traffic: add/sub/mul 96 B per element (2 x 32 B read, 32 B write), scalar ops
+// 64 B per element.  One thread per element, 32-byte coalesced loads as 2 x dwordx4,
+// grid-stride over a grid sized to keep every CU busy.  add/sub are HBM-bound; mul is one
+// Montgomery product (Fr, 8 x u32 words) per 96 B -- VALU-bound below ~16 Fr-mul/B... see
+// DESIGN.md for the measured rates.
+#include <hip/hip_runtime.h>
+
+#include "mbls_common.hpp"
+#include "mbls_field.hpp"
+
+namespace mbls {
+
+enum class VecOp { Add, Sub, Mul, ScalarMul, ScalarAdd };
+
+template <VecOp OP>
+__global__ __launch_bounds__(256) void k_vecop(uint8_t* __restrict__ out, const uint8_t* __restrict__ a,
+                                               const uint8_t* __restrict__ b, Fr s, size_t n) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) {
+        Fr y = load<FrCfg>(b + 32 * i);
+        Fr r;
+        if constexpr (OP == VecOp::Add) r = load<FrCfg>(a + 32 * i) + y;
+        if constexpr (OP == VecOp::Sub) r = load<FrCfg>(a + 32 * i) - y;
+        if constexpr (OP == VecOp::Mul) r = load<FrCfg>(a + 32 * i) * y;
+        if constexpr (OP == VecOp::ScalarMul) r = s * y;
+        if constexpr (OP == VecOp::ScalarAdd) r = s + y;
+        store<FrCfg>(out + 32 * i, r);
+    }
+}
+
+static int vec_grid(size_t n) {
+    size_t blocks = (n + 255) / 256;
+    const size_t cap = 256 * 16;  // 16 workgroups per CU, grid-stride beyond
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) blocks = 1;
+    return (int)blocks;
+}
+
+template <VecOp OP>
+static eIcicleError launch(uint8_t* out, const uint8_t* a, const uint8_t* b, const Fr& s, size_t n, hipStream_t st) {
+    if (n == 0) return MBLS_SUCCESS;
+    hipLaunchKernelGGL(k_vecop<OP>, dim3(vec_grid(n)), dim3(256), 0, st, out, a, b, s, n);
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
+}
+
+static Fr fr_from_host(const mbls_fr_t* p) {
+    Fr s;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p->limbs);
+    for (int i = 0; i < 8; ++i) s.v[i] = w[i];
+    return s;
+}
+
+// Staged wrapper with the reference run_vec_op placement semantics
+// (icicle_field_api.cu:133-192): host operands are copied in, host results copied out,
+// synchronise unless is_async.  Scratch comes from the stream arena (no per-call hipMalloc).
+template <VecOp OP>
+static eIcicleError run_vec_op(const mbls_fr_t* a, const mbls_fr_t* b, size_t size, const VecOpsConfig* cfg,
+                               mbls_fr_t* output) {
+    if (!cfg || !b || !output || (!a && OP != VecOp::ScalarMul && OP != VecOp::ScalarAdd))
+        return MBLS_INVALID_POINTER;
+    constexpr bool scalar_op = (OP == VecOp::ScalarMul || OP == VecOp::ScalarAdd);
+    if (scalar_op && !a) return MBLS_INVALID_POINTER;
+    hipStream_t st = static_cast<hipStream_t>(cfg->stream);
+    int batch = cfg->batch_size > 0 ? cfg->batch_size : 1;
+    size_t total = size * (size_t)batch;
+    if (total == 0) return MBLS_SUCCESS;
+    const size_t bytes = total * 32;
+
+    StreamCtx& ctx = stream_ctx(st);
+    std::lock_guard<std::mutex> lk(ctx.mu);
+    size_t need = 0;
+    if (!scalar_op && !cfg->is_a_on_device) need += align_up(bytes);
+    if (!cfg->is_b_on_device) need += align_up(bytes);
+    if (!cfg->is_result_on_device) need += align_up(bytes);
+    if (scalar_op && cfg->is_a_on_device) need += align_up(32 * (size_t)batch);
+    ctx.arena.reset();
+    eIcicleError er = ctx.arena.reserve(need);
+    if (er != MBLS_SUCCESS) return er;
+
+    const uint8_t* da = reinterpret_cast<const uint8_t*>(a);
+    const uint8_t* db = reinterpret_cast<const uint8_t*>(b);
+    uint8_t* dout = reinterpret_cast<uint8_t*>(output);
+    if (!scalar_op && !cfg->is_a_on_device) {
+        void* t = ctx.arena.take(bytes);
+        MBLS_TRY(hipMemcpyAsync(t, a, bytes, hipMemcpyHostToDevice, st));
+        da = static_cast<const uint8_t*>(t);
+    }
+    if (!cfg->is_b_on_device) {
+        void* t = ctx.arena.take(bytes);
+        MBLS_TRY(hipMemcpyAsync(t, b, bytes, hipMemcpyHostToDevice, st));
+        db = static_cast<const uint8_t*>(t);
+    }
+    if (!cfg->is_result_on_device) dout = static_cast<uint8_t*>(ctx.arena.take(bytes));
+
+    if (scalar_op) {
+        // one scalar per batch entry (ICICLE v4 batched scalar ops)
+        std::vector<mbls_fr_t> hs(batch);
+        if (cfg->is_a_on_device) {
+            MBLS_TRY(hipMemcpyAsync(hs.data(), a, 32 * (size_t)batch, hipMemcpyDeviceToHost, st));
+            MBLS_TRY(hipStreamSynchronize(st));
+        } else {
+            for (int k = 0; k < batch; ++k) hs[k] = a[k];
+        }
+        for (int k = 0; k < batch; ++k) {
+            er = launch<OP>(dout + (size_t)k * size * 32, nullptr, db + (size_t)k * size * 32, fr_from_host(&hs[k]),
+                            size, st);
+            if (er != MBLS_SUCCESS) return er;
+        }
+    } else {
+        er = launch<OP>(dout, da, db, Fr{}, total, st);
+        if (er != MBLS_SUCCESS) return er;
+    }
+    if (!cfg->is_result_on_device) MBLS_TRY(hipMemcpyAsync(output, dout, bytes, hipMemcpyDeviceToHost, st));
+    if (!cfg->is_async || !cfg->is_result_on_device || !cfg->is_a_on_device || !cfg->is_b_on_device)
+        MBLS_TRY(hipStreamSynchronize(st));
+    return MBLS_SUCCESS;
+}
+
+// device-pointer entry points (vec_ops.cu:393-476): no staging, enqueue only
+template <VecOp OP>
+static eIcicleError raw_vec_op(mbls_fr_t* output, const mbls_fr_t* a, const mbls_fr_t* b, int size,
+                               const VecOpsConfig* cfg) {
+    if (!output || !a || !b) return MBLS_INVALID_POINTER;
+    if (size < 0) return MBLS_INVALID_ARGUMENT;
+    hipStream_t st = cfg ? static_cast<hipStream_t>(cfg->stream) : nullptr;
+    constexpr bool scalar_op = (OP == VecOp::ScalarMul || OP == VecOp::ScalarAdd);
+    Fr s{};
+    if (scalar_op) s = fr_from_host(a);
+    eIcicleError er = launch<OP>(reinterpret_cast<uint8_t*>(output), scalar_op ? nullptr : reinterpret_cast<const uint8_t*>(a),
+                                 reinterpret_cast<const uint8_t*>(b), s, (size_t)size, st);
+    if (er != MBLS_SUCCESS) return er;
+    if (cfg && !cfg->is_async) MBLS_TRY(hipStreamSynchronize(st));
+    return MBLS_SUCCESS;
+}
+
+}  // namespace mbls
+
+using namespace mbls;
+
+extern "C" {
+
+eIcicleError bls12_381_vector_add(const mbls_fr_t* a, const mbls_fr_t* b, size_t size, const VecOpsConfig* config,
+                                  mbls_fr_t* output) {
+    return run_vec_op<VecOp::Add>(a, b, size, config, output);
+}
+eIcicleError bls12_381_vector_sub(const mbls_fr_t* a, const mbls_fr_t* b, size_t size, const VecOpsConfig* config,
+                                  mbls_fr_t* output) {
+    return run_vec_op<VecOp::Sub>(a, b, size, config, output);
+}
+eIcicleError bls12_381_vector_mul(const mbls_fr_t* a, const mbls_fr_t* b, size_t size, const VecOpsConfig* config,
+                                  mbls_fr_t* output) {
+    return run_vec_op<VecOp::Mul>(a, b, size, config, output);
+}
+eIcicleError bls12_381_scalar_mul_vec(const mbls_fr_t* scalar, const mbls_fr_t* vec, size_t size,
+                                      const VecOpsConfig* config, mbls_fr_t* output) {
+    return run_vec_op<VecOp::ScalarMul>(scalar, vec, size, config, output);
+}
+eIcicleError bls12_381_scalar_add_vec(const mbls_fr_t* scalar, const mbls_fr_t* vec, size_t size,
+                                      const VecOpsConfig* config, mbls_fr_t* output) {
+    return run_vec_op<VecOp::ScalarAdd>(scalar, vec, size, config, output);
+}
+
+eIcicleError vec_add_cuda(mbls_fr_t* output, const mbls_fr_t* a, const mbls_fr_t* b, int size, const VecOpsConfig* config) {
+    return raw_vec_op<VecOp::Add>(output, a, b, size, config);
+}
+eIcicleError vec_sub_cuda(mbls_fr_t* output, const mbls_fr_t* a, const mbls_fr_t* b, int size, const VecOpsConfig* config) {
+    return raw_vec_op<VecOp::Sub>(output, a, b, size, config);
+}
+eIcicleError vec_mul_cuda(mbls_fr_t* output, const mbls_fr_t* a, const mbls_fr_t* b, int size, const VecOpsConfig* config) {
+    return raw_vec_op<VecOp::Mul>(output, a, b, size, config);
+}
+eIcicleError scalar_mul_vec_cuda(mbls_fr_t* output, const mbls_fr_t* scalar, const mbls_fr_t* vec, int size,
+                                 const VecOpsConfig* config) {
+    return raw_vec_op<VecOp::ScalarMul>(output, scalar, vec, size, config);
+}
+eIcicleError scalar_add_vec_cuda(mbls_fr_t* output, const mbls_fr_t* scalar, const mbls_fr_t* vec, int size,
+                                 const VecOpsConfig* config) {
+    return raw_vec_op<VecOp::ScalarAdd>(output, scalar, vec, size, config);
+}
+
+}  // extern "C"

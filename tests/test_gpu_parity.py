@@ -1,0 +1,289 @@
+"""Parity of the HIP path (through the C ABI) against the oracle and the golden fixtures.
+Bit-exact for everything (integer arithmetic).  Run with -m gpu on an MI355X."""
+import numpy as np
+import pytest
+
+import helpers as H
+from helpers import pyref as pr
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def amd():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    import gpu_helpers
+    gpu_helpers.amd.lib()
+    return gpu_helpers.amd
+
+
+@pytest.fixture(scope="module")
+def gh():
+    import gpu_helpers
+    return gpu_helpers
+
+
+# ----------------------------------------------------------------------------- vecops
+@pytest.mark.parametrize("op", ["add", "sub", "mul", "scalar_mul", "scalar_add"])
+def test_vecops_golden_host(amd, op):
+    g = H.load_golden("vecops.json")
+    a = H.ints_to_limbs([H.hx(x) for x in g["a"]], 4)
+    b = H.ints_to_limbs([H.hx(x) for x in g["b"]], 4)
+    s = H.ints_to_limbs([H.hx(g["scalar"])], 4)[0]
+    out = amd.vec_op(op, s if op.startswith("scalar") else a, b)
+    assert H.limbs_to_ints(out) == [H.hx(x) for x in g[op]]
+
+
+@pytest.mark.parametrize("op", ["add", "sub", "mul"])
+def test_vecops_device_2_16_vs_oracle(amd, op):
+    import torch
+    n = 1 << 16
+    a = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    b = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(a, 0x5EED0001, montgomery=True)
+    amd.gen_scalars(b, 0x5EED0101, montgomery=True)
+    out = torch.zeros_like(a)
+    amd.vec_op(op, a, b, out=out)
+    torch.cuda.synchronize()
+    an, bn = amd.to_numpy_u64(a), amd.to_numpy_u64(b)
+    ref = np.zeros_like(an)
+    fn = {"add": H.oracle().orc_vec_add, "sub": H.oracle().orc_vec_sub, "mul": H.oracle().orc_vec_mul}[op]
+    fn(H.ptr(ref), H.ptr(an), H.ptr(bn), n)
+    assert np.array_equal(amd.to_numpy_u64(out), ref)
+
+
+def test_vecops_raw_entry_points(amd):
+    import ctypes
+    import torch
+    g = H.load_golden("vecops.json")
+    a = H.ints_to_limbs([H.hx(x) for x in g["a"]], 4)
+    b = H.ints_to_limbs([H.hx(x) for x in g["b"]], 4)
+    s = np.ascontiguousarray(H.ints_to_limbs([H.hx(g["scalar"])], 4)[0])
+    da, db = amd.torch_u64(a), amd.torch_u64(b)
+    out = torch.zeros_like(da)
+    cfg = amd.vec_config(is_a_on_device=True, is_b_on_device=True, is_result_on_device=True)
+    L = amd.lib()
+    n = a.shape[0]
+    for name, key, first in [("vec_add_cuda", "add", da), ("vec_sub_cuda", "sub", da), ("vec_mul_cuda", "mul", da),
+                             ("scalar_mul_vec_cuda", "scalar_mul", s), ("scalar_add_vec_cuda", "scalar_add", s)]:
+        amd.check(getattr(L, name)(amd._p(out), amd._p(first), amd._p(db), n, ctypes.byref(cfg)), name)
+        torch.cuda.synchronize()
+        assert H.limbs_to_ints(amd.to_numpy_u64(out)) == [H.hx(x) for x in g[key]], name
+
+
+def test_vecops_empty_and_errors(amd):
+    z = np.zeros((0, 4), dtype=np.uint64)
+    out = amd.vec_op("add", z, z)
+    assert out.shape == (0, 4)
+    with pytest.raises(amd.IcicleError) as e:
+        amd.check(amd.lib().bls12_381_vector_add(None, None, 4, None, None), "null")
+    assert e.value.code == amd.INVALID_POINTER
+
+
+# ----------------------------------------------------------------------------- NTT
+def test_ntt_golden(amd):
+    amd.ntt_init_domain()
+    g = H.load_golden("ntt.json")
+    for case in g["cases"]:
+        x = H.ints_to_limbs([H.hx(v) for v in case["input"]], 4)
+        fwd = amd.ntt(x, inverse=False)
+        inv = amd.ntt(x, inverse=True)
+        assert H.limbs_to_ints(fwd) == [H.hx(v) for v in case["forward"]], case["name"]
+        assert H.limbs_to_ints(inv) == [H.hx(v) for v in case["inverse"]], case["name"]
+
+
+@pytest.mark.parametrize("log_n", [11, 12, 15, 17, 20])
+def test_ntt_vs_oracle(amd, log_n):
+    import torch
+    amd.ntt_init_domain()
+    n = 1 << log_n
+    x = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(x, 0x5EED0002 + log_n, montgomery=True)
+    y = torch.zeros_like(x)
+    amd.ntt(x, inverse=False, out=y)
+    z = torch.zeros_like(x)
+    amd.ntt(y, inverse=True, out=z)
+    torch.cuda.synchronize()
+    xn = amd.to_numpy_u64(x)
+    ref = H.oracle_ntt(xn, log_n, False)
+    assert np.array_equal(amd.to_numpy_u64(y), ref)
+    assert np.array_equal(amd.to_numpy_u64(z), xn)  # exact round trip
+
+
+def test_ntt_batch_and_inplace(amd):
+    import torch
+    amd.ntt_init_domain()
+    log_n, batch = 10, 5
+    n = 1 << log_n
+    x = torch.zeros((n * batch, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(x, 77, montgomery=True)
+    xn = amd.to_numpy_u64(x)
+    y = x.clone()
+    amd.ntt(y, inverse=False, out=y, batch=batch)  # in place
+    torch.cuda.synchronize()
+    yn = amd.to_numpy_u64(y)
+    for b in range(batch):
+        assert np.array_equal(yn[b * n:(b + 1) * n], H.oracle_ntt(xn[b * n:(b + 1) * n], log_n, False))
+
+
+def test_ntt_coset(amd):
+    amd.ntt_init_domain()
+    g = pr.rng(5)
+    n = 64
+    xs = [g.randrange(pr.R) for _ in range(n)]
+    gen = 7
+    x = H.ints_to_limbs([pr.fr_to_mont(v) for v in xs], 4)
+    gm = np.array(pr.int_to_limbs(pr.fr_to_mont(gen), 4), dtype=np.uint64)
+    fwd = amd.ntt(x, inverse=False, coset_gen=gm)
+    expect = pr.ntt_forward([(v * pow(gen, i, pr.R)) % pr.R for i, v in enumerate(xs)])
+    assert [pr.fr_from_mont(v) for v in H.limbs_to_ints(fwd)] == expect
+    back = amd.ntt(fwd, inverse=True, coset_gen=gm)
+    assert np.array_equal(back, x)
+
+
+def test_ntt_rejects_bad_sizes(amd):
+    amd.ntt_init_domain()
+    x = np.zeros((12, 4), dtype=np.uint64)
+    with pytest.raises(amd.IcicleError) as e:
+        amd.ntt(x)
+    assert e.value.code == amd.INVALID_ARGUMENT
+
+
+# ----------------------------------------------------------------------------- MSM
+def _case_arrays(gh, case, group):
+    sc = [H.hx(s) for s in case["scalars"]]
+    pts = [H.pt_from_json(b, group) for b in case["bases"]]
+    n = len(sc)
+    s_std = H.ints_to_limbs(sc, 4) if n else np.zeros((0, 4), dtype=np.uint64)
+    s_mont = H.ints_to_limbs([pr.fr_to_mont(s) for s in sc], 4) if n else np.zeros((0, 4), dtype=np.uint64)
+    nl = 12 if group == "g1" else 24
+    b_mont = gh.affine_mont_array(group, pts) if n else np.zeros((0, nl), dtype=np.uint64)
+    return s_std, s_mont, b_mont
+
+
+@pytest.mark.parametrize("group", ["g1", "g2"])
+def test_msm_golden_icicle_semantics(amd, gh, group):
+    g = H.load_golden(f"msm_{group}.json")
+    for case in g["cases"]:
+        s_std, s_mont, b_mont = _case_arrays(gh, case, group)
+        expect = H.pt_from_json(case["result"], group)
+        r1 = amd.msm(group, s_mont, b_mont, icicle=True, scalars_mont=True, n=len(case["scalars"]))
+        assert gh.decode_icicle(group, r1[0]) == expect, case["name"]
+        r2 = amd.msm(group, s_std, b_mont, icicle=True, scalars_mont=False, n=len(case["scalars"]))
+        assert gh.decode_icicle(group, r2[0]) == expect, case["name"]
+
+
+@pytest.mark.parametrize("group", ["g1", "g2"])
+def test_msm_golden_raw_entry(amd, gh, group):
+    g = H.load_golden(f"msm_{group}.json")
+    for case in g["cases"]:
+        s_std, _, b_mont = _case_arrays(gh, case, group)
+        r = amd.msm(group, s_std, b_mont, icicle=False, n=len(case["scalars"]))
+        assert gh.decode_jacobian_mont(group, r[0]) == H.pt_from_json(case["result"], group), case["name"]
+
+
+def test_msm_window_sizes(amd, gh):
+    g = H.load_golden("msm_g1.json")
+    case = [c for c in g["cases"] if c["name"] == "random_300"][0]
+    s_std, _, b_mont = _case_arrays(gh, case, "g1")
+    expect = H.pt_from_json(case["result"], "g1")
+    for c in (2, 5, 8, 11, 13, 16, 18):
+        r = amd.msm("g1", s_std, b_mont, c=c)
+        assert gh.decode_icicle("g1", r[0]) == expect, c
+
+
+def test_msm_points_standard_form(amd, gh):
+    g = H.load_golden("msm_g1.json")
+    case = [c for c in g["cases"] if c["name"] == "random_100"][0]
+    s_std, _, _ = _case_arrays(gh, case, "g1")
+    pts = [H.pt_from_json(b, "g1") for b in case["bases"]]
+    b_std = np.array([pr.int_to_limbs(p[0], 6) + pr.int_to_limbs(p[1], 6) for p in pts], dtype=np.uint64)
+    r = amd.msm("g1", s_std, b_std, points_mont=False)
+    assert gh.decode_icicle("g1", r[0]) == H.pt_from_json(case["result"], "g1")
+
+
+def test_generated_inputs_match_oracle(amd, gh):
+    import torch
+    n = 257
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0003)
+    b1 = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b1, 0x5EED0013)
+    b2 = torch.zeros((64, 24), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g2", b2, 0x5EED0015)
+    torch.cuda.synchronize()
+    o = H.oracle()
+    rs = np.zeros((n, 4), dtype=np.uint64)
+    o.orc_gen_scalars(H.ptr(rs), 0x5EED0003, n)
+    r1 = np.zeros((n, 12), dtype=np.uint64)
+    o.orc_gen_g1_bases(H.ptr(r1), 0x5EED0013, n, 0)
+    r2 = np.zeros((64, 24), dtype=np.uint64)
+    o.orc_gen_g2_bases(H.ptr(r2), 0x5EED0015, 64, 0)
+    assert np.array_equal(amd.to_numpy_u64(s), rs)
+    assert np.array_equal(amd.to_numpy_u64(b1), r1)
+    assert np.array_equal(amd.to_numpy_u64(b2), r2)
+
+
+@pytest.mark.parametrize("log_n", [10, 14, 16])
+def test_msm_g1_device_vs_oracle(amd, gh, log_n):
+    import torch
+    n = 1 << log_n
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0003 + log_n, montgomery=True)
+    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 0x5EED0013 + log_n)
+    out = torch.zeros((1, 18), dtype=torch.int64, device="cuda")
+    amd.msm("g1", s, b, scalars_mont=True, out=out)
+    torch.cuda.synchronize()
+    s_std = np.zeros((n, 4), dtype=np.uint64)
+    H.oracle().orc_gen_scalars(H.ptr(s_std), 0x5EED0003 + log_n, n)
+    ref = H.oracle_msm("g1", s_std, amd.to_numpy_u64(b))
+    assert gh.decode_icicle("g1", amd.to_numpy_u64(out)[0]) == H.g1_from_affine_mont(ref)
+
+
+def test_msm_precompute_factor(amd, gh):
+    g = H.load_golden("msm_g1.json")
+    case = [c for c in g["cases"] if c["name"] == "random_300"][0]
+    s_std, _, b_mont = _case_arrays(gh, case, "g1")
+    n = s_std.shape[0]
+    expect = H.pt_from_json(case["result"], "g1")
+    for c, factor in [(8, 2), (8, 4), (10, 26), (13, 5)]:
+        pre = amd.precompute_bases("g1", b_mont, factor, n, c=c)
+        r = amd.msm("g1", s_std, pre, c=c, precompute_factor=factor, n=n)
+        assert gh.decode_icicle("g1", r[0]) == expect, (c, factor)
+
+
+def test_msm_batch(amd, gh):
+    g = H.load_golden("msm_g1.json")
+    cases = [c for c in g["cases"] if c["name"] in ("random_16", "max_digit_patterns")]
+    # shared bases: same bases, different scalars
+    base_case = [c for c in g["cases"] if c["name"] == "random_16"][0]
+    s_std, _, b_mont = _case_arrays(gh, base_case, "g1")
+    n = s_std.shape[0]
+    rng = pr.rng(11)
+    batches = [s_std] + [H.ints_to_limbs([rng.randrange(pr.R) for _ in range(n)], 4) for _ in range(3)]
+    allsc = np.ascontiguousarray(np.concatenate(batches))
+    r = amd.msm("g1", allsc, b_mont, batch=4, n=n)
+    pts = [H.pt_from_json(p, "g1") for p in base_case["bases"]]
+    for k in range(4):
+        expect = pr.msm_shared_doubling(H.limbs_to_ints(batches[k]), pts)
+        assert gh.decode_icicle("g1", r[k]) == expect, k
+    assert cases
+
+
+def test_msm_sum_jacobian_and_convert(amd, gh):
+    import torch
+    # partial results of a split MSM summed on device == full MSM (the multi-GPU reduction)
+    g = H.load_golden("msm_g1.json")
+    case = [c for c in g["cases"] if c["name"] == "random_300"][0]
+    s_std, _, b_mont = _case_arrays(gh, case, "g1")
+    parts = torch.zeros((3, 18), dtype=torch.int64, device="cuda")
+    for k, (lo, hi) in enumerate([(0, 100), (100, 230), (230, 300)]):
+        r = amd.msm("g1", np.ascontiguousarray(s_std[lo:hi]), np.ascontiguousarray(b_mont[lo:hi]), icicle=False)
+        parts[k] = amd.torch_u64(r[0])
+    tot = torch.zeros((1, 18), dtype=torch.int64, device="cuda")
+    amd.sum_jacobian("g1", parts, tot)
+    amd.jacobian_to_icicle("g1", tot)
+    torch.cuda.synchronize()
+    assert gh.decode_icicle("g1", amd.to_numpy_u64(tot)[0]) == H.pt_from_json(case["result"], "g1")

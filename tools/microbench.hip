@@ -1,0 +1,135 @@
+// tools/microbench.hip -- gfx950 roof probes used for the design decisions in DESIGN.md:
+//   * v_mad_u64_u32 issue rate (the multiprecision multiply primitive),
+//   * Fr / Fq Montgomery-multiply rate of mbls_field.hpp,
+//   * streaming copy bandwidth (achievable HBM roof).
+// Build: hipcc --offload-arch=gfx950 -O3 -I../midnight-bls12-381-cuda_amd/csrc microbench.hip -o microbench
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include "mbls_field.hpp"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+using namespace mbls;
+
+__global__ void k_mad(uint64_t* out, uint32_t seed, int iters) {
+    uint32_t x = seed ^ threadIdx.x;
+    uint64_t acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = x + k;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = (uint64_t)(uint32_t)acc[k] * (x + k) + (acc[k] >> 32);
+    }
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s ^= acc[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <class C, int CH>
+__global__ void k_mont(uint32_t* out, const uint32_t* in, int iters) {
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    Fp<C> x[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        x[k] = load<C>(in + C::N * ((tid + k) & 1023));
+    }
+    Fp<C> y = load<C>(in + C::N * 1024);
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < CH; ++k) x[k] = x[k] * y;
+    }
+    Fp<C> s = x[0];
+#pragma unroll
+    for (int k = 1; k < CH; ++k) s = s + x[k];
+    store<C>(out + C::N * tid, s);
+}
+
+__global__ void k_copy(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
+int main() {
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    printf("device %s CUs %d clock %d kHz\n", prop.gcnArchName, prop.multiProcessorCount, prop.clockRate);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float ms;
+
+    // ---- mad rate
+    {
+        int blocks = 256 * 8, threads = 256, iters = 4096;
+        uint64_t* out;
+        CK(hipMalloc(&out, sizeof(uint64_t) * blocks * threads));
+        hipLaunchKernelGGL(k_mad, blocks, threads, 0, 0, out, 1u, 16);
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_mad, blocks, threads, 0, 0, out, 1u, iters);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        double mads = (double)blocks * threads * iters * 8;
+        printf("mad_u64_u32: %.3f ms, %.3f Tmad/s (%.1f mad/clk/CU @2.4GHz)\n", ms, mads / ms / 1e9,
+               mads / (ms * 1e-3) / 256 / 2.4e9);
+        CK(hipFree(out));
+    }
+    // ---- Montgomery mul rate
+    {
+        uint32_t* in;
+        uint32_t* out;
+        int blocks = 256 * 8, threads = 256, iters = 256;
+        CK(hipMalloc(&in, 4 * 12 * 2048));
+        CK(hipMalloc(&out, 4 * 12 * (size_t)blocks * threads));
+        uint32_t* h = (uint32_t*)malloc(4 * 12 * 2048);
+        for (int i = 0; i < 12 * 2048; ++i) h[i] = (uint32_t)rand();
+        for (int i = 0; i < 2048; ++i) { h[12 * i + 11] &= 0x0fffffff; }
+        // keep Fr-view values < r too: top word of each 8-word group small
+        for (int i = 0; i < 12 * 2048 / 8; ++i) h[8 * i + 7] &= 0x0fffffff;
+        CK(hipMemcpy(in, h, 4 * 12 * 2048, hipMemcpyHostToDevice));
+#define RUN_MONT(C, CH)                                                                          \
+        {                                                                                        \
+            hipLaunchKernelGGL((k_mont<C, CH>), blocks, threads, 0, 0, out, in, 4);              \
+            CK(hipDeviceSynchronize());                                                          \
+            CK(hipEventRecord(e0));                                                              \
+            hipLaunchKernelGGL((k_mont<C, CH>), blocks, threads, 0, 0, out, in, iters);          \
+            CK(hipEventRecord(e1));                                                              \
+            CK(hipEventSynchronize(e1));                                                         \
+            CK(hipEventElapsedTime(&ms, e0, e1));                                                \
+            double muls = (double)blocks * threads * iters * CH;                                 \
+            printf(#C " mont_mul x%d chains: %.3f ms, %.2f Gmul/s\n", CH, ms, muls / ms / 1e6);  \
+        }
+        RUN_MONT(FrCfg, 1)
+        RUN_MONT(FrCfg, 2)
+        RUN_MONT(FrCfg, 4)
+        RUN_MONT(FqCfg, 1)
+        RUN_MONT(FqCfg, 2)
+        CK(hipFree(in));
+        CK(hipFree(out));
+        free(h);
+    }
+    // ---- copy bandwidth
+    {
+        size_t bytes = (size_t)1 << 30;
+        uint4 *a, *b;
+        CK(hipMalloc(&a, bytes));
+        CK(hipMalloc(&b, bytes));
+        CK(hipMemset(a, 1, bytes));
+        size_t n = bytes / 16;
+        for (int rep = 0; rep < 3; ++rep) {
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL(k_copy, 256 * 16, 256, 0, 0, b, a, n);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&ms, e0, e1));
+        }
+        printf("copy 1 GiB: %.3f ms, %.2f TB/s (read+write)\n", ms, 2.0 * bytes / ms / 1e9);
+        CK(hipFree(a));
+        CK(hipFree(b));
+    }
+    return 0;
+}
