@@ -217,6 +217,14 @@ eIcicleError mbls_g2_sum_jacobian(const mbls_g2_projective_t* points_device, int
 eIcicleError mbls_g1_jacobian_to_icicle(mbls_g1_projective_t* points_device, int count, void* stream);
 eIcicleError mbls_g2_jacobian_to_icicle(mbls_g2_projective_t* points_device, int count, void* stream);
 
+/* Stage profiler (tracing): hipEvent pairs recorded on the caller's
+ * stream around each pipeline stage ("msm.accumulate", "ntt.pass", ...) when enabled
+ * (or MBLS_PROFILE=1).  read() synchronises the recorded events and returns, per stage,
+ * the total milliseconds and the number of recorded launches. */
+void mbls_profile_enable(int on);
+void mbls_profile_reset(void);
+int mbls_profile_read(const char** names, double* total_ms, long* counts, int max);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,7 @@ EXPORTED = [
     "scalar_add_vec_cuda",
     "mbls_version", "mbls_error_string", "mbls_gen_scalars", "mbls_gen_g1_bases", "mbls_gen_g2_bases",
     "mbls_g1_sum_jacobian", "mbls_g2_sum_jacobian", "mbls_g1_jacobian_to_icicle", "mbls_g2_jacobian_to_icicle",
+    "mbls_profile_enable", "mbls_profile_reset", "mbls_profile_read",
 ]
 
 _LIB = None
@@ -114,8 +115,30 @@ def lib():
     L.mbls_default_msm_config.restype = MSMConfig
     L.mbls_default_ntt_config.restype = NTTConfig
     L.mbls_default_vec_ops_config.restype = VecOpsConfig
+    L.mbls_profile_enable.argtypes = [ctypes.c_int]
+    L.mbls_profile_enable.restype = None
+    L.mbls_profile_reset.argtypes = []
+    L.mbls_profile_reset.restype = None
+    L.mbls_profile_read.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                    ctypes.POINTER(ctypes.c_long), ctypes.c_int]
+    L.mbls_profile_read.restype = ctypes.c_int
     _LIB = L
     return L
+
+
+def profile(enable=True):
+    lib().mbls_profile_enable(1 if enable else 0)
+    lib().mbls_profile_reset()
+
+
+def profile_read():
+    """{stage: (total_ms, launches)} since the last profile()/reset"""
+    n = 64
+    names = (ctypes.c_char_p * n)()
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_long * n)()
+    k = lib().mbls_profile_read(names, ms, cnt, n)
+    return {names[i].decode(): (ms[i], cnt[i]) for i in range(min(k, n))}
 
 
 def check(code, what):

@@ -5,6 +5,8 @@
 
 #include <map>
 #include <memory>
+#include <string>
+#include <vector>
 
 #include "mbls_common.hpp"
 
@@ -85,9 +87,72 @@ bool is_device_pointer(const void* p) {
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+static std::mutex g_prof_mu;
+static int g_prof_on = -1;
+struct ProfEntry {
+    std::string name;
+    hipEvent_t a, b;
+};
+static std::vector<ProfEntry> g_prof_pending;
+static std::map<std::string, std::pair<double, long>> g_prof_sum;
+
+bool profile_enabled() {
+    if (g_prof_on < 0) {
+        const char* s = getenv("MBLS_PROFILE");
+        g_prof_on = (s && *s && *s != '0') ? 1 : 0;
+    }
+    return g_prof_on == 1;
+}
+
+void profile_record(const char* name, hipEvent_t a, hipEvent_t b) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_pending.push_back({name, a, b});
+}
+
+static void profile_drain() {
+    for (auto& e : g_prof_pending) {
+        float ms = 0.f;
+        (void)hipEventSynchronize(e.b);
+        (void)hipEventElapsedTime(&ms, e.a, e.b);
+        auto& s = g_prof_sum[e.name];
+        s.first += ms;
+        s.second += 1;
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    g_prof_pending.clear();
+}
+
 }  // namespace mbls
 
 extern "C" {
+
+void mbls_profile_enable(int on) {
+    std::lock_guard<std::mutex> lk(mbls::g_prof_mu);
+    mbls::g_prof_on = on ? 1 : 0;
+}
+
+void mbls_profile_reset(void) {
+    std::lock_guard<std::mutex> lk(mbls::g_prof_mu);
+    mbls::profile_drain();
+    mbls::g_prof_sum.clear();
+}
+
+/* Fills up to `max` entries: names (static until the next reset), total ms, call counts.
+ * Returns the number of stages recorded. */
+int mbls_profile_read(const char** names, double* total_ms, long* counts, int max) {
+    std::lock_guard<std::mutex> lk(mbls::g_prof_mu);
+    mbls::profile_drain();
+    int i = 0;
+    for (auto& kv : mbls::g_prof_sum) {
+        if (i >= max) break;
+        names[i] = kv.first.c_str();
+        total_ms[i] = kv.second.first;
+        counts[i] = kv.second.second;
+        ++i;
+    }
+    return (int)mbls::g_prof_sum.size();
+}
 
 const char* mbls_version(void) { return "bls12_381_mi355x 0.1 (gfx950)"; }
 

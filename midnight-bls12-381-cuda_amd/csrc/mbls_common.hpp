@@ -61,4 +61,28 @@ inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 // is `p` a device (or managed) pointer?  Used only for defensive validation.
 bool is_device_pointer(const void* p);
 
+// Stage profiler: when enabled (mbls_profile_enable / MBLS_PROFILE=1) a ProfScope records a
+// hipEvent pair on the stream around the enclosed launches; mbls_profile_read() sums the
+// elapsed times per stage name.  Disabled: one branch, no events.
+bool profile_enabled();
+void profile_record(const char* name, hipEvent_t a, hipEvent_t b);
+struct ProfScope {
+    const char* name;
+    hipStream_t st;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(const char* n, hipStream_t s) : name(n), st(s) {
+        if (profile_enabled()) {
+            (void)hipEventCreate(&a);
+            (void)hipEventCreate(&b);
+            (void)hipEventRecord(a, st);
+        }
+    }
+    ~ProfScope() {
+        if (a) {
+            (void)hipEventRecord(b, st);
+            profile_record(name, a, b);
+        }
+    }
+};
+
 }  // namespace mbls

@@ -390,19 +390,34 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint8_t* windows = (uint8_t*)arena.take(z.windows);
     if (!windows) return MBLS_ALLOCATION_FAILED;
 
-    MBLS_TRY(hipMemsetAsync(counts, 0, (size_t)TB * 4, st));
-    eIcicleError er = launch_digits(scalars, scalars_mont, n, P, keys, vals, counts, st);
-    if (er != MBLS_SUCCESS) return er;
-    if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) return er;
-    MBLS_TRY(hipMemcpyAsync(cursor, offsets, (size_t)TB * 4, hipMemcpyDeviceToDevice, st));
-    if ((er = launch_chunk_counts(counts, nchunks, TB, st)) != MBLS_SUCCESS) return er;
-    if ((er = scan_exclusive(nchunks, chunk_off, TB, tmp, st)) != MBLS_SUCCESS) return er;
-    if ((er = launch_scatter(keys, vals, NC, cursor, sorted, st)) != MBLS_SUCCESS) return er;
-    if ((er = launch_chunk_owner(chunk_off, TB, owner, st)) != MBLS_SUCCESS) return er;
-    // the chunk count is data dependent: launch the bound, extra threads exit
-    hipLaunchKernelGGL(k_accumulate<F>, dim3((max_chunks + 255) / 256), dim3(256), 0, st, sorted, offsets, chunk_off,
-                       owner, TB, max_chunks, bases, partials);
-    hipLaunchKernelGGL(k_bucket_sum<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials, buckets);
+    ProfScope prof_all("msm.total", st);
+    eIcicleError er;
+    {
+        ProfScope ps("msm.digits", st);
+        MBLS_TRY(hipMemsetAsync(counts, 0, (size_t)TB * 4, st));
+        er = launch_digits(scalars, scalars_mont, n, P, keys, vals, counts, st);
+        if (er != MBLS_SUCCESS) return er;
+    }
+    {
+        ProfScope ps("msm.sort", st);
+        if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) return er;
+        MBLS_TRY(hipMemcpyAsync(cursor, offsets, (size_t)TB * 4, hipMemcpyDeviceToDevice, st));
+        if ((er = launch_chunk_counts(counts, nchunks, TB, st)) != MBLS_SUCCESS) return er;
+        if ((er = scan_exclusive(nchunks, chunk_off, TB, tmp, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_scatter(keys, vals, NC, cursor, sorted, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_chunk_owner(chunk_off, TB, owner, st)) != MBLS_SUCCESS) return er;
+    }
+    {
+        // the chunk count is data dependent: launch the bound, extra threads exit
+        ProfScope ps("msm.accumulate", st);
+        hipLaunchKernelGGL(k_accumulate<F>, dim3((max_chunks + 255) / 256), dim3(256), 0, st, sorted, offsets,
+                           chunk_off, owner, TB, max_chunks, bases, partials);
+    }
+    {
+        ProfScope ps("msm.bucket_sum", st);
+        hipLaunchKernelGGL(k_bucket_sum<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials, buckets);
+    }
+    ProfScope ps_red("msm.reduce", st);
     // recursive running-sum reduction
     const uint8_t* V = buckets;
     size_t lvoff = 0;
@@ -420,7 +435,10 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         lvoff += (size_t)m_out * P.Wg;
     }
     hipLaunchKernelGGL(k_window_horner<F>, dim3((P.Wg + 63) / 64), dim3(64), 0, st, sums, P.levels, P.Wg, windows);
-    hipLaunchKernelGGL(k_final<F>, dim3(1), dim3(64), 0, st, windows, P.Wg, P.c, result);
+    {
+        ProfScope ps("msm.final", st);
+        hipLaunchKernelGGL(k_final<F>, dim3(1), dim3(64), 0, st, windows, P.Wg, P.c, result);
+    }
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }

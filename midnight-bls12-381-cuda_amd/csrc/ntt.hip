@@ -34,6 +34,7 @@ namespace mbls {
 static constexpr int NTT_TILE_LOG = 10;
 static constexpr int NTT_TILE = 1 << NTT_TILE_LOG;  // elements per workgroup tile
 static constexpr int NTT_THREADS = 256;
+static constexpr int NTT_PASS_STAGES = 8;
 
 // canonical 2^32-th root of unity, Montgomery (bls12_381_constants.h:127-130)
 static const uint64_t ROOT_2_32_MONT[4] = {0xb9b58d8c5f0e466aULL, 0x5b1b4c801819d7ecULL, 0x0af53ae352a31e64ULL,
@@ -311,10 +312,13 @@ eIcicleError ntt_device(uint8_t* out, const uint8_t* in, int log_n, bool inverse
         MBLS_TRY(hipGetLastError());
         return MBLS_SUCCESS;
     }
-    // split the k stages into passes of <= NTT_TILE_LOG stages
-    int npass = (log_n + NTT_TILE_LOG - 1) / NTT_TILE_LOG;
+    // split the k stages into passes of <= NTT_PASS_STAGES stages (tile rows), so that a tile
+    // keeps >= 4 adjacent columns (>= 128-byte contiguous row segments in HBM)
+    int npass = (log_n + NTT_PASS_STAGES - 1) / NTT_PASS_STAGES;
     int s0 = 0;
+    ProfScope prof_t("ntt.transform", st);
     for (int p = 0; p < npass; ++p) {
+        ProfScope prof_p("ntt.pass", st);
         int remaining = log_n - s0;
         int L = (remaining + (npass - p) - 1) / (npass - p);
         bool first = (p == 0);

@@ -17,7 +17,8 @@ LIB = os.path.join(PKG, "lib", "libbls12_381_mi355x.so")
 def header_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    names = re.findall(r"\b(?:eIcicleError|MSMConfig|NTTConfig|VecOpsConfig|const char\*)\s+(\w+)\s*\(", src)
+    names = re.findall(r"^(?:eIcicleError|MSMConfig|NTTConfig|VecOpsConfig|const char\*|void|int)\s+(\w+)\s*\(",
+                       src, flags=re.M)
     return sorted(set(names))
 
 

@@ -1,8 +1,5 @@
 #!/bin/bash
-# run the GPU parity suite + smoke on the box (one process per step, each time-limited)
-set -o pipefail
+# run the GPU parity suite on the box (verbose per-test lines to a file so progress is visible)
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider "$@" > gpurun_out/pytest_gpu.txt 2>&1
-rc=$?
-tail -40 gpurun_out/pytest_gpu.txt
-exit $rc
+timeout -k 10 1000 python -m pytest tests -m gpu -x -v -p no:cacheprovider "$@" 2>&1 | tee gpurun_out/pytest_gpu.txt | grep -E "PASSED|FAILED|ERROR|passed|failed|error" 
+exit ${PIPESTATUS[0]}
