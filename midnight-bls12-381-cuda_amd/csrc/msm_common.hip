@@ -9,7 +9,9 @@
 
 namespace mbls {
 
-// window size: the reference's size classes (msm.cuh:115-133)
+// window size: the reference's size classes (msm.cuh:115-133) except c = 15, where
+// 17 * 15 = 255 leaves an 18th window holding only the final carry -- one bucket with about
+// half of all points (measured: 1.3 s of serial bucket summation at 2^20).  c = 16 instead.
 static int optimal_c(long long n) {
     if (n <= (1 << 8)) return 7;
     if (n <= (1 << 10)) return 8;
@@ -17,7 +19,6 @@ static int optimal_c(long long n) {
     if (n <= (1 << 14)) return 12;
     if (n <= (1 << 16)) return 13;
     if (n <= (1 << 18)) return 14;
-    if (n <= (1 << 20)) return 15;
     return 16;
 }
 
@@ -56,7 +57,7 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p) {
 // 1. digits: one thread per scalar
 // ------------------------------------------------------------------------------------
 template <bool MONT>
-__global__ __launch_bounds__(256) void k_digits(const uint8_t* __restrict__ scalars, uint32_t n, int c, int W, int Wg,
+__global__ __launch_bounds__(256) void k_digits(const uint8_t* __restrict__ scalars, uint32_t n, int c, int W, int Wg, uint32_t F,
                                                 uint32_t B, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                 uint32_t* __restrict__ counts) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -86,12 +87,22 @@ __global__ __launch_bounds__(256) void k_digits(const uint8_t* __restrict__ scal
         }
         const size_t o = (size_t)w * n + i;
         const int f = w / Wg, wl = w % Wg;
-        if (v == 0) {
-            keys[o] = INVALID_KEY;
-        } else {
-            const uint32_t key = (uint32_t)wl * B + (v - 1);
-            keys[o] = key;
-            vals[o] = (((uint32_t)f * n + i) << 1) | sign;
+        // precomputed bases are point-major: [P_i, 2^l P_i, ..., 2^((F-1) l) P_i] (core/msm.rs:164-165)
+        uint32_t key = INVALID_KEY;
+        if (v != 0) {
+            key = (uint32_t)wl * B + (v - 1);
+            vals[o] = ((i * F + (uint32_t)f) << 1) | sign;
+        }
+        keys[o] = key;
+        // histogram: one atomic per wave when the whole wave hits one bucket (adversarial
+        // inputs: equal scalars), else one per lane
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+        const uint64_t active = __ballot(1);
+        const uint64_t same = __ballot(key == k0);
+        if (same == active) {
+            if (k0 != INVALID_KEY && __lane_id() == (uint32_t)__builtin_ctzll(active))
+                atomicAdd(&counts[k0], (uint32_t)__popcll(active));
+        } else if (key != INVALID_KEY) {
             atomicAdd(&counts[key], 1u);
         }
     }
@@ -103,9 +114,11 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
                            uint32_t* vals, uint32_t* counts, hipStream_t st) {
     dim3 g((n + 255) / 256);
     if (mont)
-        hipLaunchKernelGGL(k_digits<true>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, P.B, keys, vals, counts);
+        hipLaunchKernelGGL(k_digits<true>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, (uint32_t)P.F, P.B, keys,
+                           vals, counts);
     else
-        hipLaunchKernelGGL(k_digits<false>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, P.B, keys, vals, counts);
+        hipLaunchKernelGGL(k_digits<false>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, (uint32_t)P.F, P.B, keys,
+                           vals, counts);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }
@@ -194,12 +207,21 @@ eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint3
     return MBLS_SUCCESS;
 }
 
+// chunks per bucket; nchunks[m] receives the maximum (drives the heavy-bucket tree passes)
 __global__ void k_chunk_counts(const uint32_t* __restrict__ counts, uint32_t* __restrict__ nchunks, uint32_t m) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < m) nchunks[b] = (counts[b] + CHUNK - 1) / CHUNK;
+    uint32_t c = 0;
+    if (b < m) {
+        c = (counts[b] + CHUNK - 1) / CHUNK;
+        nchunks[b] = c;
+    }
+    // wave max, one atomic per wave
+    for (int d = 32; d > 0; d >>= 1) c = max(c, (uint32_t)__shfl_xor(c, d, 64));
+    if ((threadIdx.x & 63) == 0 && c > 1) atomicMax(&nchunks[m], c);
 }
 
 eIcicleError launch_chunk_counts(const uint32_t* counts, uint32_t* nchunks, uint32_t m, hipStream_t st) {
+    MBLS_TRY(hipMemsetAsync(nchunks + m, 0, 4, st));
     hipLaunchKernelGGL(k_chunk_counts, dim3((m + 255) / 256), dim3(256), 0, st, counts, nchunks, m);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
@@ -212,7 +234,20 @@ __global__ __launch_bounds__(256) void k_scatter(const uint32_t* __restrict__ ke
                                                  size_t total, uint32_t* __restrict__ cursor, uint32_t* __restrict__ sorted) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= total) return;
-    uint32_t k = keys[i];
+    const uint32_t k = keys[i];
+    // wave-uniform bucket (adversarial inputs): one atomic reserves the wave's slots
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(k);
+    const uint64_t active = __ballot(1);
+    if (__ballot(k == k0) == active) {
+        if (k0 == INVALID_KEY) return;
+        uint32_t base = 0;
+        const uint32_t leader = (uint32_t)__builtin_ctzll(active);
+        if (__lane_id() == leader) base = atomicAdd(&cursor[k0], (uint32_t)__popcll(active));
+        base = __shfl(base, leader, 64);
+        const uint32_t rank = (uint32_t)__popcll(active & ((1ull << __lane_id()) - 1));
+        sorted[base + rank] = vals[i];
+        return;
+    }
     if (k == INVALID_KEY) return;
     uint32_t pos = atomicAdd(&cursor[k], 1u);
     sorted[pos] = vals[i];

@@ -88,18 +88,41 @@ __global__ __launch_bounds__(256) void k_accumulate(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------------------------------------
-// 5. bucket sums from chunk partials
+// 5. bucket sums from chunk partials: in-place tree over the chunks of each bucket with
+//    fan-in TREE_FANIN per pass, so a bucket holding many chunks (adversarial inputs) costs
+//    log passes instead of one serial thread.  Passes past the largest bucket exit at once
+//    (maxc = max chunks per bucket, computed on device).
 // ------------------------------------------------------------------------------------
+static constexpr int TREE_FANIN = 4;
+
 template <class F>
-__global__ __launch_bounds__(256) void k_bucket_sum(const uint32_t* __restrict__ chunk_off, uint32_t m,
-                                                    const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
+__global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict__ chunk_off,
+                                                     const uint32_t* __restrict__ owner, uint32_t TB,
+                                                     uint32_t max_chunks, const uint32_t* __restrict__ maxc,
+                                                     uint32_t step, uint8_t* __restrict__ partials) {
+    if (step >= *maxc) return;
+    uint32_t ch = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch >= max_chunks || ch >= chunk_off[TB]) return;
+    const uint32_t b = owner[ch];
+    const uint32_t j = ch - chunk_off[b];
+    const uint32_t cnt = chunk_off[b + 1] - chunk_off[b];
+    if (j % (TREE_FANIN * step) != 0 || j + step >= cnt) return;
+    Jacobian<F> acc = load_jac<F>(partials, ch);
+    for (int g = 1; g < TREE_FANIN; ++g) {
+        uint32_t o = j + g * step;
+        if (o >= cnt) break;
+        acc = jac_add(acc, load_jac<F>(partials, (size_t)ch + g * step));
+    }
+    store_jac<F>(partials, ch, acc);
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void k_bucket_gather(const uint32_t* __restrict__ chunk_off, uint32_t m,
+                                                       const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
     uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
-    Jacobian<F> acc = Jacobian<F>::inf();
-    if (k1 > k0) acc = load_jac<F>(partials, k0);
-    for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<F>(partials, k));
-    store_jac<F>(buckets, b, acc);
+    store_jac<F>(buckets, b, k1 > k0 ? load_jac<F>(partials, k0) : Jacobian<F>::inf());
 }
 
 // ------------------------------------------------------------------------------------
@@ -302,17 +325,18 @@ __global__ void k_gen_bases(uint8_t* out, uint64_t seed, size_t n) {
     store_affine<F>(out, i, jac_to_affine(jac_mul_u32(g, k.v)));
 }
 
-// precomputed bases: out[f*n + i] = 2^(shift*f) * P_i (Montgomery affine)
+// precomputed bases, point-major as ICICLE / core/msm.rs:164-165 document:
+// out[i*factor + f] = 2^(shift*f) * P_i (Montgomery affine)
 template <class F>
 __global__ void k_precompute(const uint8_t* in, uint8_t* out, size_t n, int factor, int shift) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     Affine<F> a = load_affine<F>(in, i);
-    store_affine<F>(out, i, a);
+    store_affine<F>(out, i * factor, a);
     Jacobian<F> p = Jacobian<F>::from_affine(a);
     for (int f = 1; f < factor; ++f) {
         for (int k = 0; k < shift; ++k) p = jac_dbl(p);
-        store_affine<F>(out, (size_t)f * n + i, jac_to_affine(p));
+        store_affine<F>(out, i * factor + f, jac_to_affine(p));
     }
 }
 
@@ -415,7 +439,13 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     }
     {
         ProfScope ps("msm.bucket_sum", st);
-        hipLaunchKernelGGL(k_bucket_sum<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials, buckets);
+        // worst case: every contribution of a window group in one bucket
+        const uint32_t max_per_bucket = (uint32_t)(((size_t)n * P.F + CHUNK - 1) / CHUNK);
+        for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
+            hipLaunchKernelGGL(k_bucket_tree<F>, dim3((max_chunks + 255) / 256), dim3(256), 0, st, chunk_off, owner,
+                               TB, max_chunks, nchunks + TB, step, partials);
+        hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials,
+                           buckets);
     }
     ProfScope ps_red("msm.reduce", st);
     // recursive running-sum reduction

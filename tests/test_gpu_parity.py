@@ -242,6 +242,26 @@ def test_msm_g1_device_vs_oracle(amd, gh, log_n):
     assert gh.decode_icicle("g1", amd.to_numpy_u64(out)[0]) == H.g1_from_affine_mont(ref)
 
 
+@pytest.mark.parametrize("c", [0, 15])
+def test_msm_adversarial_heavy_buckets(amd, gh, c):
+    """all scalars equal (every window's contributions land in ONE bucket) and c = 15 (whose
+    top window holds only carries): heavy buckets must still reduce exactly."""
+    import torch
+    n = 1 << 13
+    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 99)
+    s_one = H.ints_to_limbs([pr.R - 12345] * n, 4)
+    out = amd.msm("g1", amd.torch_u64(s_one), b, icicle=True, c=c, n=n)
+    bn = amd.to_numpy_u64(b)
+    ref = H.oracle_msm("g1", s_one, bn)
+    assert gh.decode_icicle("g1", out[0]) == H.g1_from_affine_mont(ref)
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 1234)
+    out = amd.msm("g1", s, b, icicle=True, c=c, n=n)
+    ref = H.oracle_msm("g1", amd.to_numpy_u64(s), bn)
+    assert gh.decode_icicle("g1", out[0]) == H.g1_from_affine_mont(ref)
+
+
 def test_msm_precompute_factor(amd, gh):
     g = H.load_golden("msm_g1.json")
     case = [c for c in g["cases"] if c["name"] == "random_300"][0]
