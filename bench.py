@@ -45,8 +45,9 @@ def main():
     import torch
     import torch.distributed as dist
     import bls12_381_amd as amd
+    import sharded_msm
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world =int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -79,7 +80,7 @@ def main():
         amd.msm("g1", scalars, bases, icicle=False, scalars_mont=True, out=partial, stream=stream,
                 is_async=True, n=n)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, partial)
+            sharded_msm.gather_partials(partial, world, dist, out=gathered)
             amd.sum_jacobian("g1", gathered, total, stream=stream)
 
     for _ in range(args.warmup):
