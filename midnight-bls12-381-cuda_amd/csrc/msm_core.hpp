@@ -31,6 +31,7 @@
 
 #include "mbls_common.hpp"
 #include "mbls_curve.hpp"
+#include "mbls_rowfield.hpp"
 
 namespace mbls {
 
@@ -126,7 +127,31 @@ __global__ __launch_bounds__(256) void k_bucket_gather(const uint32_t* __restric
 }
 
 // ------------------------------------------------------------------------------------
-// 6. one level of the recursive running-sum reduction.
+// Serial phases run on ROW-SLICED arithmetic (mbls_rowfield.hpp): one logical thread =
+// one 16-lane row holding a field element limb-per-lane, so a serial chain of additions
+// costs ~150 instead of ~1.3 K dependent instructions per product.  `rid` = row index.
+// ------------------------------------------------------------------------------------
+template <class F>
+using RJac = Jacobian<typename RowOf<F>::type>;
+
+template <class F>
+MBLS_DEV RJac<F> rload_jac(const uint8_t* base, size_t idx) {
+    using RO = RowOf<F>;
+    const size_t q = idx * 3 * RO::FQS;
+    return {RO::ld(base, q), RO::ld(base, q + RO::FQS), RO::ld(base, q + 2 * RO::FQS)};
+}
+template <class F>
+MBLS_DEV void rstore_jac(uint8_t* base, size_t idx, const RJac<F>& a) {
+    using RO = RowOf<F>;
+    const size_t q = idx * 3 * RO::FQS;
+    RO::st(base, q, a.x);
+    RO::st(base, q + RO::FQS, a.y);
+    RO::st(base, q + 2 * RO::FQS, a.z);
+}
+MBLS_DEV uint32_t row_id() { return (blockIdx.x * blockDim.x + threadIdx.x) >> 4; }
+
+// ------------------------------------------------------------------------------------
+// 6. one level of the recursive running-sum reduction (one row per segment).
 //   in:  V[w * m_in + k], k < m_in, weight (k + off)
 //   out: T[w * m_out + q], R[w * m_out + q], m_out = ceil(m_in / SEG)
 // Single jac_add call site: the loop alternates the R and S updates.
@@ -135,12 +160,12 @@ template <class F>
 __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict__ V, uint32_t m_in, int Wg, int off,
                                                       uint8_t* __restrict__ T, uint8_t* __restrict__ R) {
     const uint32_t m_out = (m_in + SEG - 1) / SEG;
-    uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t tid = row_id();
     if (tid >= m_out * (uint32_t)Wg) return;
     const uint32_t w = tid / m_out, q = tid % m_out;
     const uint32_t k0 = q * SEG;
     const uint32_t k1 = min(k0 + SEG, m_in);  // exclusive
-    Jacobian<F> Racc = Jacobian<F>::inf(), Sacc = Jacobian<F>::inf();
+    RJac<F> Racc = RJac<F>::inf(), Sacc = RJac<F>::inf();
     // walk t = k1-1 .. k0: R += V_t; S += R unless (t - k0 + off) == 0
     int steps = 2 * (int)(k1 - k0);
     uint32_t t = k1 - 1;
@@ -151,9 +176,9 @@ __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict_
             --t;
             continue;
         }
-        Jacobian<F> x = r_step ? Racc : Sacc;
-        Jacobian<F> y = r_step ? load_jac<F>(V, (size_t)w * m_in + t) : Racc;
-        Jacobian<F> z = jac_add(x, y);
+        RJac<F> x = r_step ? Racc : Sacc;
+        RJac<F> y = r_step ? rload_jac<F>(V, (size_t)w * m_in + t) : Racc;
+        RJac<F> z = jac_add(x, y);
         if (r_step) {
             Racc = z;
         } else {
@@ -162,60 +187,53 @@ __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict_
             --t;
         }
     }
-    store_jac<F>(T, tid, Sacc);
-    store_jac<F>(R, tid, Racc);
+    rstore_jac<F>(T, tid, Sacc);
+    rstore_jac<F>(R, tid, Racc);
 }
 
-// per-window sum of `m` points: V[w * m + k] -> out[w]; one block per window
+// per-window sum of `m` points: V[w * m + k] -> out[w]; one block (16 rows) per window
 template <class F>
-__global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V, uint32_t m, uint8_t* __restrict__ out,
-                                                  size_t out_stride_elems) {
-    __shared__ __attribute__((aligned(16))) uint8_t sh[64 * 3 * sizeof(F)];
+__global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V, uint32_t m, uint8_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[16 * 3 * sizeof(F)];
     const uint32_t w = blockIdx.x;
-    Jacobian<F> acc = Jacobian<F>::inf();
-    // 256 threads sweep sequentially, then waves fold via LDS (64 partials), then one wave
-    for (uint32_t k = threadIdx.x; k < m; k += 256) acc = jac_add(acc, load_jac<F>(V, (size_t)w * m + k));
-    // fold the 4 waves into 64 slots
-    for (int wave = 3; wave >= 0; --wave) {
-        if ((int)(threadIdx.x >> 6) == wave) {
-            if (wave < 3) acc = jac_add(acc, load_jac<F>(sh, threadIdx.x & 63));
-            store_jac<F>(sh, threadIdx.x & 63, acc);
+    const uint32_t r = threadIdx.x >> 4;  // row in block
+    RJac<F> acc = RJac<F>::inf();
+    for (uint32_t k = r; k < m; k += 16) acc = jac_add(acc, rload_jac<F>(V, (size_t)w * m + k));
+    rstore_jac<F>(sh, r, acc);
+    __syncthreads();
+    for (uint32_t s = 8; s > 0; s >>= 1) {
+        if (r < s) {
+            acc = jac_add(acc, rload_jac<F>(sh, r + s));
+            rstore_jac<F>(sh, r, acc);
         }
         __syncthreads();
     }
-    for (int s = 32; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            acc = jac_add(acc, load_jac<F>(sh, threadIdx.x + s));
-            store_jac<F>(sh, threadIdx.x, acc);
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) store_jac<F>(out, (size_t)w * out_stride_elems, acc);
+    if (r == 0) rstore_jac<F>(out, w, acc);
 }
 
-// G_w = sumT[0] + SEG*(sumT[1] + SEG*(...)): sums laid out sums[l * Wg + w]
+// G_w = sumT[0] + SEG*(sumT[1] + SEG*(...)): sums laid out sums[l * Wg + w]; one row per window
 template <class F>
 __global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, int Wg, uint8_t* __restrict__ windows) {
-    int w = blockIdx.x * blockDim.x + threadIdx.x;
+    const int w = (int)row_id();
     if (w >= Wg) return;
-    Jacobian<F> acc = load_jac<F>(sums, (size_t)(levels - 1) * Wg + w);
+    RJac<F> acc = rload_jac<F>(sums, (size_t)(levels - 1) * Wg + w);
     for (int l = levels - 2; l >= 0; --l) {
         for (int k = 0; k < SEG_LOG; ++k) acc = jac_dbl(acc);
-        acc = jac_add(acc, load_jac<F>(sums, (size_t)l * Wg + w));
+        acc = jac_add(acc, rload_jac<F>(sums, (size_t)l * Wg + w));
     }
-    store_jac<F>(windows, w, acc);
+    rstore_jac<F>(windows, w, acc);
 }
 
-// final fold over window groups: sum_w 2^(c w) G_w
+// final fold over window groups: sum_w 2^(c w) G_w  (one row)
 template <class F>
 __global__ void k_final(const uint8_t* __restrict__ windows, int Wg, int c, uint8_t* __restrict__ result) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    Jacobian<F> acc = load_jac<F>(windows, Wg - 1);
+    if (row_id() != 0) return;
+    RJac<F> acc = rload_jac<F>(windows, Wg - 1);
     for (int w = Wg - 2; w >= 0; --w) {
         for (int k = 0; k < c; ++k) acc = jac_dbl(acc);
-        acc = jac_add(acc, load_jac<F>(windows, w));
+        acc = jac_add(acc, rload_jac<F>(windows, w));
     }
-    store_jac<F>(result, 0, acc);
+    rstore_jac<F>(result, 0, acc);
 }
 
 template <class F>
@@ -258,31 +276,44 @@ __global__ void k_points_to_mont(uint8_t* pts, size_t n) {
 
 // Jacobian Montgomery -> ICICLE standard projective (x, y, 1); identity (0, 1, 0)
 // (reference icicle_curve_api.cu:134-229)
+MBLS_DEV RFq from_mont_f(const RFq& a) { return from_mont(a); }
+MBLS_DEV RFq2 from_mont_f(const RFq2& a) { return {from_mont(a.c0), from_mont(a.c1)}; }
+template <>
+MBLS_DEV RFq one_std<RFq>() {
+    return {rowdpp::lane16() == 0 ? 1u : 0u};
+}
+template <>
+MBLS_DEV RFq2 one_std<RFq2>() {
+    return {one_std<RFq>(), RFq::zero()};
+}
+
+// one row per point (a Fermat inversion is a ~570-product serial chain)
 template <class F>
 __global__ void k_jac_to_icicle(uint8_t* pts, int count) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    using RF = typename RowOf<F>::type;
+    const int i = (int)row_id();
     if (i >= count) return;
-    Jacobian<F> p = load_jac<F>(pts, i);
-    Jacobian<F> o;
+    RJac<F> p = rload_jac<F>(pts, i);
+    RJac<F> o;
     if (p.is_inf()) {
-        o.x = F::zero();
-        o.y = one_std<F>();
-        o.z = F::zero();
+        o.x = RF::zero();
+        o.y = one_std<RF>();
+        o.z = RF::zero();
     } else {
-        Affine<F> a = jac_to_affine(p);
+        Affine<RF> a = jac_to_affine(p);
         o.x = from_mont_f(a.x);
         o.y = from_mont_f(a.y);
-        o.z = one_std<F>();
+        o.z = one_std<RF>();
     }
-    store_jac<F>(pts, i, o);
+    rstore_jac<F>(pts, i, o);
 }
 
 template <class F>
 __global__ void k_sum_jac(const uint8_t* pts, int count, uint8_t* out) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    Jacobian<F> acc = Jacobian<F>::inf();
-    for (int i = 0; i < count; ++i) acc = jac_add(acc, load_jac<F>(pts, i));
-    store_jac<F>(out, 0, acc);
+    if (row_id() != 0) return;
+    RJac<F> acc = RJac<F>::inf();
+    for (int i = 0; i < count; ++i) acc = jac_add(acc, rload_jac<F>(pts, i));
+    rstore_jac<F>(out, 0, acc);
 }
 
 template <class F>
@@ -456,15 +487,14 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         uint32_t m_out = (m_in + SEG - 1) / SEG;
         uint8_t* T = levelT + lvoff * JAC;
         uint8_t* R = levelR + lvoff * JAC;
-        uint32_t threads = m_out * (uint32_t)P.Wg;
+        uint32_t threads = m_out * (uint32_t)P.Wg * 16;  // one 16-lane row per segment
         hipLaunchKernelGGL(k_reduce_level<F>, dim3((threads + 255) / 256), dim3(256), 0, st, V, m_in, P.Wg,
                            l == 0 ? 1 : 0, T, R);
-        hipLaunchKernelGGL(k_tree_sum<F>, dim3(P.Wg), dim3(256), 0, st, T, m_out, sums + (size_t)l * P.Wg * JAC,
-                           (size_t)1);
+        hipLaunchKernelGGL(k_tree_sum<F>, dim3(P.Wg), dim3(256), 0, st, T, m_out, sums + (size_t)l * P.Wg * JAC);
         V = R;
         lvoff += (size_t)m_out * P.Wg;
     }
-    hipLaunchKernelGGL(k_window_horner<F>, dim3((P.Wg + 63) / 64), dim3(64), 0, st, sums, P.levels, P.Wg, windows);
+    hipLaunchKernelGGL(k_window_horner<F>, dim3((P.Wg * 16 + 63) / 64), dim3(64), 0, st, sums, P.levels, P.Wg, windows);
     {
         ProfScope ps("msm.final", st);
         hipLaunchKernelGGL(k_final<F>, dim3(1), dim3(64), 0, st, windows, P.Wg, P.c, result);
@@ -535,7 +565,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
         if (er != MBLS_SUCCESS) return er;
     }
     if (icicle_semantics) {
-        hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch + 63) / 64), dim3(64), 0, st, d_r, batch);
+        hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch * 16 + 63) / 64), dim3(64), 0, st, d_r, batch);
         MBLS_TRY(hipGetLastError());
     }
     MBLS_TRY(hipMemcpyAsync(results, d_r, JAC * (size_t)batch,
