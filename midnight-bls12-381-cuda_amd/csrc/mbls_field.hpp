@@ -162,9 +162,10 @@ MBLS_DEV Fp<C> dbl(const Fp<C>& a) {
 }
 
 // Montgomery product a*b*2^(-32N) mod m -- no-carry CIOS, every word step is
-// v_mad_u64_u32 + one 64-bit add.
+// v_mad_u64_u32 + one 64-bit add.  Reference implementation; the hot paths use the
+// product-scanning form in mbls_fips.hpp (operator* below), 1.4-1.5x faster on gfx950.
 template <class C>
-MBLS_DEV Fp<C> operator*(const Fp<C>& a, const Fp<C>& b) {
+MBLS_DEV Fp<C> mul_cios(const Fp<C>& a, const Fp<C>& b) {
     constexpr int N = C::N;
     uint32_t t[N];
 #pragma unroll
@@ -191,9 +192,18 @@ MBLS_DEV Fp<C> operator*(const Fp<C>& a, const Fp<C>& b) {
     return r;
 }
 
+}  // namespace mbls
+#include "mbls_fips.hpp"
+namespace mbls {
+
+template <class C>
+MBLS_DEV Fp<C> operator*(const Fp<C>& a, const Fp<C>& b) {
+    return fips::mul(a, b);
+}
+
 template <class C>
 MBLS_DEV Fp<C> sqr(const Fp<C>& a) {
-    return a * a;
+    return fips::sqr(a);
 }
 
 template <class C>

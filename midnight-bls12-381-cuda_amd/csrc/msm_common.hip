@@ -46,7 +46,8 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p) {
     while (true) {
         if (p.levels >= MAX_LEVELS) return MBLS_INVALID_ARGUMENT;
         p.level_m[p.levels++] = m;
-        uint32_t mo = (m + SEG - 1) / SEG;
+        const uint32_t seg = level_seg(p.levels - 1);
+        uint32_t mo = (m + seg - 1) / seg;
         if (mo <= 1) break;
         m = mo;
     }

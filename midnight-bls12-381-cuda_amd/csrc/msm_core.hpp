@@ -37,8 +37,10 @@ namespace mbls {
 
 static constexpr uint32_t INVALID_KEY = 0xffffffffu;
 static constexpr int CHUNK = 16;  // max points per accumulation thread
-static constexpr int SEG = 16;    // inputs per reduction segment (power of two)
+static constexpr int SEG = 16;    // inputs per reduction segment, levels >= 1 (row-sliced)
 static constexpr int SEG_LOG = 4;
+static constexpr int SEG0 = 4;    // level 0 (one segment per lane): short chains, many lanes
+static constexpr int SEG0_LOG = 2;
 static constexpr int MAX_MSM_LOG = 26;
 static constexpr int SCAN_BLOCK = 1024;
 static constexpr int MAX_LEVELS = 8;
@@ -101,12 +103,13 @@ __global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ owner, uint32_t TB,
                                                      uint32_t max_chunks, const uint32_t* __restrict__ maxc,
                                                      uint32_t step, uint8_t* __restrict__ partials) {
-    if (step >= *maxc) return;
+    if (*maxc <= TREE_FANIN || step >= *maxc) return;  // only heavy buckets remain
     uint32_t ch = blockIdx.x * blockDim.x + threadIdx.x;
     if (ch >= max_chunks || ch >= chunk_off[TB]) return;
     const uint32_t b = owner[ch];
     const uint32_t j = ch - chunk_off[b];
     const uint32_t cnt = chunk_off[b + 1] - chunk_off[b];
+    if (cnt <= TREE_FANIN) return;  // summed by k_bucket_small
     if (j % (TREE_FANIN * step) != 0 || j + step >= cnt) return;
     Jacobian<F> acc = load_jac<F>(partials, ch);
     for (int g = 1; g < TREE_FANIN; ++g) {
@@ -117,13 +120,29 @@ __global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict_
     store_jac<F>(partials, ch, acc);
 }
 
+// common case: one thread per bucket sums its <= TREE_FANIN chunk partials (all lanes busy)
 template <class F>
-__global__ __launch_bounds__(256) void k_bucket_gather(const uint32_t* __restrict__ chunk_off, uint32_t m,
-                                                       const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
+__global__ __launch_bounds__(256) void k_bucket_small(const uint32_t* __restrict__ chunk_off, uint32_t m,
+                                                      const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
-    uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
-    store_jac<F>(buckets, b, k1 > k0 ? load_jac<F>(partials, k0) : Jacobian<F>::inf());
+    const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
+    if (k1 - k0 > TREE_FANIN) return;  // heavy: tree passes + k_bucket_gather
+    Jacobian<F> acc = Jacobian<F>::inf();
+    if (k1 > k0) acc = load_jac<F>(partials, k0);
+    for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<F>(partials, k));
+    store_jac<F>(buckets, b, acc);
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void k_bucket_gather(const uint32_t* __restrict__ chunk_off, uint32_t m,
+                                                       const uint32_t* __restrict__ maxc,
+                                                       const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
+    if (*maxc <= TREE_FANIN) return;
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= m) return;
+    const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
+    if (k1 - k0 > TREE_FANIN) store_jac<F>(buckets, b, load_jac<F>(partials, k0));
 }
 
 // ------------------------------------------------------------------------------------
@@ -151,21 +170,42 @@ MBLS_DEV void rstore_jac(uint8_t* base, size_t idx, const RJac<F>& a) {
 MBLS_DEV uint32_t row_id() { return (blockIdx.x * blockDim.x + threadIdx.x) >> 4; }
 
 // ------------------------------------------------------------------------------------
-// 6. one level of the recursive running-sum reduction (one row per segment).
+// 6. one level of the recursive running-sum reduction.
 //   in:  V[w * m_in + k], k < m_in, weight (k + off)
-//   out: T[w * m_out + q], R[w * m_out + q], m_out = ceil(m_in / SEG)
+//   out: T[w * m_out + q], R[w * m_out + q], m_out = ceil(m_in / seg)
+// Level 0 has plenty of segments and runs one segment per LANE (scalar arithmetic, short
+// segments); the later, narrower levels run one segment per ROW (row-sliced arithmetic).
 // Single jac_add call site: the loop alternates the R and S updates.
 // ------------------------------------------------------------------------------------
+template <class F, bool ROW>
+struct RedIO;
 template <class F>
-__global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict__ V, uint32_t m_in, int Wg, int off,
-                                                      uint8_t* __restrict__ T, uint8_t* __restrict__ R) {
-    const uint32_t m_out = (m_in + SEG - 1) / SEG;
-    const uint32_t tid = row_id();
+struct RedIO<F, false> {
+    using J = Jacobian<F>;
+    MBLS_DEV static uint32_t id() { return blockIdx.x * blockDim.x + threadIdx.x; }
+    MBLS_DEV static J ld(const uint8_t* b, size_t i) { return load_jac<F>(b, i); }
+    MBLS_DEV static void st(uint8_t* b, size_t i, const J& v) { store_jac<F>(b, i, v); }
+};
+template <class F>
+struct RedIO<F, true> {
+    using J = RJac<F>;
+    MBLS_DEV static uint32_t id() { return row_id(); }
+    MBLS_DEV static J ld(const uint8_t* b, size_t i) { return rload_jac<F>(b, i); }
+    MBLS_DEV static void st(uint8_t* b, size_t i, const J& v) { rstore_jac<F>(b, i, v); }
+};
+
+template <class F, bool ROW>
+__global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict__ V, uint32_t m_in, uint32_t seg, int Wg,
+                                                      int off, uint8_t* __restrict__ T, uint8_t* __restrict__ R) {
+    using IO = RedIO<F, ROW>;
+    using J = typename IO::J;
+    const uint32_t m_out = (m_in + seg - 1) / seg;
+    const uint32_t tid = IO::id();
     if (tid >= m_out * (uint32_t)Wg) return;
     const uint32_t w = tid / m_out, q = tid % m_out;
-    const uint32_t k0 = q * SEG;
-    const uint32_t k1 = min(k0 + SEG, m_in);  // exclusive
-    RJac<F> Racc = RJac<F>::inf(), Sacc = RJac<F>::inf();
+    const uint32_t k0 = q * seg;
+    const uint32_t k1 = min(k0 + seg, m_in);  // exclusive
+    J Racc = J::inf(), Sacc = J::inf();
     // walk t = k1-1 .. k0: R += V_t; S += R unless (t - k0 + off) == 0
     int steps = 2 * (int)(k1 - k0);
     uint32_t t = k1 - 1;
@@ -176,9 +216,9 @@ __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict_
             --t;
             continue;
         }
-        RJac<F> x = r_step ? Racc : Sacc;
-        RJac<F> y = r_step ? rload_jac<F>(V, (size_t)w * m_in + t) : Racc;
-        RJac<F> z = jac_add(x, y);
+        J x = r_step ? Racc : Sacc;
+        J y = r_step ? IO::ld(V, (size_t)w * m_in + t) : Racc;
+        J z = jac_add(x, y);
         if (r_step) {
             Racc = z;
         } else {
@@ -187,18 +227,22 @@ __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict_
             --t;
         }
     }
-    rstore_jac<F>(T, tid, Sacc);
-    rstore_jac<F>(R, tid, Racc);
+    IO::st(T, tid, Sacc);
+    IO::st(R, tid, Racc);
 }
 
-// per-window sum of `m` points: V[w * m + k] -> out[w]; one block (16 rows) per window
+// tree-sum stage: block b of window w sums V[w*m + k], k in [b*16*per_row, ...): each of the
+// 16 rows sums `per_row` consecutive points, then a 4-level LDS tree.  out[w*nblk + b].
+static constexpr int TREE_PER_ROW = 8;
 template <class F>
-__global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V, uint32_t m, uint8_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V, uint32_t m, uint32_t nblk,
+                                                  uint8_t* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint8_t sh[16 * 3 * sizeof(F)];
-    const uint32_t w = blockIdx.x;
+    const uint32_t w = blockIdx.x / nblk, blk = blockIdx.x % nblk;
     const uint32_t r = threadIdx.x >> 4;  // row in block
     RJac<F> acc = RJac<F>::inf();
-    for (uint32_t k = r; k < m; k += 16) acc = jac_add(acc, rload_jac<F>(V, (size_t)w * m + k));
+    const uint32_t k0 = (blk * 16 + r) * TREE_PER_ROW;
+    for (uint32_t k = k0; k < min(k0 + TREE_PER_ROW, m); ++k) acc = jac_add(acc, rload_jac<F>(V, (size_t)w * m + k));
     rstore_jac<F>(sh, r, acc);
     __syncthreads();
     for (uint32_t s = 8; s > 0; s >>= 1) {
@@ -208,17 +252,19 @@ __global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V,
         }
         __syncthreads();
     }
-    if (r == 0) rstore_jac<F>(out, w, acc);
+    if (r == 0) rstore_jac<F>(out, blockIdx.x, acc);
 }
 
-// G_w = sumT[0] + SEG*(sumT[1] + SEG*(...)): sums laid out sums[l * Wg + w]; one row per window
+// G_w = sumT[0] + seg0*(sumT[1] + SEG*(sumT[2] + ...)): sums[l * Wg + w]; one row per window
 template <class F>
-__global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, int Wg, uint8_t* __restrict__ windows) {
+__global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, int Wg, int seg0_log,
+                                uint8_t* __restrict__ windows) {
     const int w = (int)row_id();
     if (w >= Wg) return;
     RJac<F> acc = rload_jac<F>(sums, (size_t)(levels - 1) * Wg + w);
     for (int l = levels - 2; l >= 0; --l) {
-        for (int k = 0; k < SEG_LOG; ++k) acc = jac_dbl(acc);
+        const int dbls = (l == 0) ? seg0_log : SEG_LOG;
+        for (int k = 0; k < dbls; ++k) acc = jac_dbl(acc);
         acc = jac_add(acc, rload_jac<F>(sums, (size_t)l * Wg + w));
     }
     rstore_jac<F>(windows, w, acc);
@@ -386,11 +432,15 @@ struct GroupTraits<Fq2> {
 };
 
 struct MsmScratchSizes {
-    size_t keys, vals, sorted, words, tmp, owner, partials, buckets, levelT, levelR, sums, windows;
+    size_t keys, vals, sorted, words, tmp, owner, partials, buckets, levelT, levelR, sums, windows, treetmp;
     size_t total() const {
-        return keys + vals + sorted + 5 * words + tmp + owner + partials + buckets + levelT + levelR + sums + windows;
+        return keys + vals + sorted + 5 * words + tmp + owner + partials + buckets + levelT + levelR + sums + windows +
+               2 * treetmp;
     }
 };
+
+inline uint32_t level_seg(int l) { return l == 0 ? SEG0 : SEG; }
+inline uint32_t tree_blocks(uint32_t m) { return (m + 16 * TREE_PER_ROW - 1) / (16 * TREE_PER_ROW); }
 
 inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, uint32_t max_chunks) {
     MsmScratchSizes z;
@@ -403,12 +453,17 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, uint32_t 
     z.owner = align_up((size_t)max_chunks * 4);
     z.partials = align_up((size_t)max_chunks * jac);
     z.buckets = align_up((size_t)P.TB * jac);
-    size_t lv = 0;
-    for (int l = 0; l < P.levels; ++l) lv += (P.level_m[l] + SEG - 1) / SEG;
+    size_t lv = 0, maxblk = 1;
+    for (int l = 0; l < P.levels; ++l) {
+        uint32_t mo = (P.level_m[l] + level_seg(l) - 1) / level_seg(l);
+        lv += mo;
+        maxblk = maxblk > tree_blocks(mo) ? maxblk : tree_blocks(mo);
+    }
     z.levelT = align_up(lv * P.Wg * jac);
     z.levelR = align_up(lv * P.Wg * jac);
     z.sums = align_up((size_t)P.levels * P.Wg * jac);
     z.windows = align_up((size_t)P.Wg * jac);
+    z.treetmp = align_up(maxblk * P.Wg * jac);
     return z;
 }
 
@@ -443,7 +498,9 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint8_t* levelR = (uint8_t*)arena.take(z.levelR);
     uint8_t* sums = (uint8_t*)arena.take(z.sums);
     uint8_t* windows = (uint8_t*)arena.take(z.windows);
-    if (!windows) return MBLS_ALLOCATION_FAILED;
+    uint8_t* tree_a = (uint8_t*)arena.take(z.treetmp);
+    uint8_t* tree_b = (uint8_t*)arena.take(z.treetmp);
+    if (!tree_b) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
@@ -472,29 +529,54 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         ProfScope ps("msm.bucket_sum", st);
         // worst case: every contribution of a window group in one bucket
         const uint32_t max_per_bucket = (uint32_t)(((size_t)n * P.F + CHUNK - 1) / CHUNK);
-        for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
-            hipLaunchKernelGGL(k_bucket_tree<F>, dim3((max_chunks + 255) / 256), dim3(256), 0, st, chunk_off, owner,
-                               TB, max_chunks, nchunks + TB, step, partials);
-        hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials,
+        hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials,
                            buckets);
+        if (max_per_bucket > TREE_FANIN) {
+            for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
+                hipLaunchKernelGGL(k_bucket_tree<F>, dim3((max_chunks + 255) / 256), dim3(256), 0, st, chunk_off,
+                                   owner, TB, max_chunks, nchunks + TB, step, partials);
+            hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB,
+                               nchunks + TB, partials, buckets);
+        }
     }
     ProfScope ps_red("msm.reduce", st);
     // recursive running-sum reduction
     const uint8_t* V = buckets;
     size_t lvoff = 0;
     for (int l = 0; l < P.levels; ++l) {
-        uint32_t m_in = P.level_m[l];
-        uint32_t m_out = (m_in + SEG - 1) / SEG;
+        const uint32_t m_in = P.level_m[l];
+        const uint32_t seg = level_seg(l);
+        const uint32_t m_out = (m_in + seg - 1) / seg;
         uint8_t* T = levelT + lvoff * JAC;
         uint8_t* R = levelR + lvoff * JAC;
-        uint32_t threads = m_out * (uint32_t)P.Wg * 16;  // one 16-lane row per segment
-        hipLaunchKernelGGL(k_reduce_level<F>, dim3((threads + 255) / 256), dim3(256), 0, st, V, m_in, P.Wg,
-                           l == 0 ? 1 : 0, T, R);
-        hipLaunchKernelGGL(k_tree_sum<F>, dim3(P.Wg), dim3(256), 0, st, T, m_out, sums + (size_t)l * P.Wg * JAC);
+        if (l == 0) {  // one segment per lane
+            const uint32_t threads = m_out * (uint32_t)P.Wg;
+            hipLaunchKernelGGL((k_reduce_level<F, false>), dim3((threads + 255) / 256), dim3(256), 0, st, V, m_in, seg,
+                               P.Wg, 1, T, R);
+        } else {  // one segment per 16-lane row
+            const uint32_t threads = m_out * (uint32_t)P.Wg * 16;
+            hipLaunchKernelGGL((k_reduce_level<F, true>), dim3((threads + 255) / 256), dim3(256), 0, st, V, m_in, seg,
+                               P.Wg, 0, T, R);
+        }
+        // sum of this level's T per window: tree stages until one point per window
+        const uint8_t* src = T;
+        uint32_t m = m_out;
+        uint8_t* pp[2] = {tree_a, tree_b};
+        int flip = 0;
+        while (true) {
+            const uint32_t nblk = tree_blocks(m);
+            uint8_t* dst = (nblk == 1) ? sums + (size_t)l * P.Wg * JAC : pp[flip];
+            hipLaunchKernelGGL(k_tree_sum<F>, dim3(P.Wg * nblk), dim3(256), 0, st, src, m, nblk, dst);
+            if (nblk == 1) break;
+            src = dst;
+            m = nblk;
+            flip ^= 1;
+        }
         V = R;
         lvoff += (size_t)m_out * P.Wg;
     }
-    hipLaunchKernelGGL(k_window_horner<F>, dim3((P.Wg * 16 + 63) / 64), dim3(64), 0, st, sums, P.levels, P.Wg, windows);
+    hipLaunchKernelGGL(k_window_horner<F>, dim3((P.Wg * 16 + 63) / 64), dim3(64), 0, st, sums, P.levels, P.Wg, SEG0_LOG,
+                       windows);
     {
         ProfScope ps("msm.final", st);
         hipLaunchKernelGGL(k_final<F>, dim3(1), dim3(64), 0, st, windows, P.Wg, P.c, result);

@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include "mbls_field.hpp"
+#include "mbls_fips.hpp"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
@@ -27,7 +28,30 @@ __global__ void k_mad(uint64_t* out, uint32_t seed, int iters) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
-template <class C, int CH>
+// OP 0: CIOS operator*, 1: fips::mul, 2: fips::sqr
+template <class C, int OP>
+MBLS_DEV Fp<C> opf(const Fp<C>& a, const Fp<C>& b) {
+    if constexpr (OP == 0) return a * b;
+    if constexpr (OP == 1) return fips::mul(a, b);
+    return fips::sqr(a);
+}
+
+// correctness: compare fips mul/sqr with CIOS on a*b and a*a; count mismatches
+template <class C>
+__global__ void k_check(unsigned* bad, const uint32_t* in) {
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    Fp<C> a = load<C>(in + C::N * (tid & 1023));
+    Fp<C> b = load<C>(in + C::N * ((tid * 7 + 3) & 1023));
+    for (int it = 0; it < 8; ++it) {
+        Fp<C> r0 = a * b, r1 = fips::mul(a, b), s0 = a * a, s1 = fips::sqr(a);
+        if (!(r0 == r1)) atomicAdd(bad, 1u);
+        if (!(s0 == s1)) atomicAdd(bad + 1, 1u);
+        a = r0;
+        b = s0 + b;
+    }
+}
+
+template <class C, int CH, int OP = 0>
 __global__ void k_mont(uint32_t* out, const uint32_t* in, int iters) {
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     Fp<C> x[CH];
@@ -38,7 +62,7 @@ __global__ void k_mont(uint32_t* out, const uint32_t* in, int iters) {
     Fp<C> y = load<C>(in + C::N * 1024);
     for (int i = 0; i < iters; ++i) {
 #pragma unroll
-        for (int k = 0; k < CH; ++k) x[k] = x[k] * y;
+        for (int k = 0; k < CH; ++k) x[k] = opf<C, OP>(x[k], y);
     }
     Fp<C> s = x[0];
 #pragma unroll
@@ -91,23 +115,41 @@ int main() {
         // keep Fr-view values < r too: top word of each 8-word group small
         for (int i = 0; i < 12 * 2048 / 8; ++i) h[8 * i + 7] &= 0x0fffffff;
         CK(hipMemcpy(in, h, 4 * 12 * 2048, hipMemcpyHostToDevice));
-#define RUN_MONT(C, CH)                                                                          \
-        {                                                                                        \
-            hipLaunchKernelGGL((k_mont<C, CH>), blocks, threads, 0, 0, out, in, 4);              \
-            CK(hipDeviceSynchronize());                                                          \
-            CK(hipEventRecord(e0));                                                              \
-            hipLaunchKernelGGL((k_mont<C, CH>), blocks, threads, 0, 0, out, in, iters);          \
-            CK(hipEventRecord(e1));                                                              \
-            CK(hipEventSynchronize(e1));                                                         \
-            CK(hipEventElapsedTime(&ms, e0, e1));                                                \
-            double muls = (double)blocks * threads * iters * CH;                                 \
-            printf(#C " mont_mul x%d chains: %.3f ms, %.2f Gmul/s\n", CH, ms, muls / ms / 1e6);  \
+#define RUN_MONT(C, CH, OP)                                                                          \
+        {                                                                                            \
+            hipLaunchKernelGGL((k_mont<C, CH, OP>), blocks, threads, 0, 0, out, in, 4);              \
+            CK(hipDeviceSynchronize());                                                              \
+            CK(hipEventRecord(e0));                                                                  \
+            hipLaunchKernelGGL((k_mont<C, CH, OP>), blocks, threads, 0, 0, out, in, iters);          \
+            CK(hipEventRecord(e1));                                                                  \
+            CK(hipEventSynchronize(e1));                                                             \
+            CK(hipEventElapsedTime(&ms, e0, e1));                                                    \
+            double muls = (double)blocks * threads * iters * CH;                                     \
+            printf(#C " op%d x%d chains: %.3f ms, %.2f Gmul/s\n", OP, CH, ms, muls / ms / 1e6);      \
         }
-        RUN_MONT(FrCfg, 1)
-        RUN_MONT(FrCfg, 2)
-        RUN_MONT(FrCfg, 4)
-        RUN_MONT(FqCfg, 1)
-        RUN_MONT(FqCfg, 2)
+        {
+            unsigned* bad;
+            CK(hipMalloc(&bad, 16));
+            CK(hipMemset(bad, 0, 16));
+            hipLaunchKernelGGL(k_check<FrCfg>, 256, 256, 0, 0, bad, in);
+            hipLaunchKernelGGL(k_check<FqCfg>, 256, 256, 0, 0, bad + 2, in);
+            unsigned hb[4];
+            CK(hipMemcpy(hb, bad, 16, hipMemcpyDeviceToHost));
+            printf("fips check mismatches: Fr mul %u sqr %u | Fq mul %u sqr %u (of %d each)\n", hb[0], hb[1], hb[2],
+                   hb[3], 256 * 256 * 8);
+        }
+        RUN_MONT(FrCfg, 1, 0)
+        RUN_MONT(FrCfg, 2, 0)
+        RUN_MONT(FrCfg, 1, 1)
+        RUN_MONT(FrCfg, 2, 1)
+        RUN_MONT(FrCfg, 1, 2)
+        RUN_MONT(FrCfg, 2, 2)
+        RUN_MONT(FqCfg, 1, 0)
+        RUN_MONT(FqCfg, 2, 0)
+        RUN_MONT(FqCfg, 1, 1)
+        RUN_MONT(FqCfg, 2, 1)
+        RUN_MONT(FqCfg, 1, 2)
+        RUN_MONT(FqCfg, 2, 2)
         CK(hipFree(in));
         CK(hipFree(out));
         free(h);
