@@ -78,6 +78,16 @@ StreamCtx& stream_ctx(hipStream_t s) {
     return *it->second;
 }
 
+eIcicleError StreamCtx::ensure_side(size_t nevents) {
+    if (!side) MBLS_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    while (events.size() < nevents) {
+        hipEvent_t e;
+        MBLS_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        events.push_back(e);
+    }
+    return MBLS_SUCCESS;
+}
+
 bool is_device_pointer(const void* p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {

@@ -50,7 +50,13 @@ class Arena {
 struct StreamCtx {
     std::mutex mu;
     Arena arena;
+    // side stream for latency-bound work that overlaps the main chain (MSM tree sums);
+    // forked from / joined back into the caller's stream with events, so callers see one
+    // stream-ordered operation
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> events;
     explicit StreamCtx(hipStream_t s) : arena(s) {}
+    eIcicleError ensure_side(size_t nevents);
 };
 StreamCtx& stream_ctx(hipStream_t s);
 

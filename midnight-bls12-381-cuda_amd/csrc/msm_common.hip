@@ -22,14 +22,16 @@ static int optimal_c(long long n) {
     return 16;
 }
 
-eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p) {
+eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, bool allow_glv) {
     int c = cfg->c > 0 ? cfg->c : optimal_c(n);
     if (c < 2 || c > 20) return MBLS_INVALID_ARGUMENT;
     int bits = cfg->bitsize > 0 ? cfg->bitsize : 255;
     if (bits > 256) return MBLS_INVALID_ARGUMENT;
-    // signed digits need one bit of headroom for the top carry
-    int W = (bits + 1 + c - 1) / c;
     int F = cfg->precompute_factor > 0 ? cfg->precompute_factor : 1;
+    // GLV (G1, no precomputed table, full-width scalars): two half-width digit streams < 2^127
+    p.glv = allow_glv && F == 1 && bits > 128;
+    // signed digits need one bit of headroom for the top carry
+    int W = p.glv ? (128 + c - 1) / c : (bits + 1 + c - 1) / c;
     if (F > W) F = W;
     int Wg = (W + F - 1) / F;
     p.c = c;
@@ -38,20 +40,54 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p) {
     p.Wg = Wg;
     p.B = 1u << (c - 1);
     p.TB = (uint32_t)Wg * p.B;
-    p.contributions = (size_t)n * W;
-    if ((size_t)n * F >= (1u << 31)) return MBLS_INVALID_ARGUMENT;
-    // reduction levels: level 0 has B inputs, each level divides by SEG, the last has 1 output
+    p.pts = (size_t)n * (p.glv ? 2 : F);  // point indices per window (P_i then phi(P_i))
+    p.contributions = (size_t)n * W * (p.glv ? 2 : 1);
+    if (p.pts >= (1u << 31)) return MBLS_INVALID_ARGUMENT;
+    // reduction levels: level 0 has B inputs, level l divides by 2^seg_log[l], the last has
+    // one output.  MBLS_ROW_SEG_LOG (tuning) overrides the row-level segment length.
+    static const int row_log = [] {
+        const char* e = getenv("MBLS_ROW_SEG_LOG");
+        int v = e ? atoi(e) : SEG_LOG;
+        return v >= 1 && v <= 6 ? v : SEG_LOG;
+    }();
     p.levels = 0;
     uint32_t m = p.B;
     while (true) {
         if (p.levels >= MAX_LEVELS) return MBLS_INVALID_ARGUMENT;
+        p.seg_log[p.levels] = (uint8_t)(p.levels == 0 ? SEG0_LOG : row_log);
         p.level_m[p.levels++] = m;
-        const uint32_t seg = level_seg(p.levels - 1);
+        const uint32_t seg = p.seg(p.levels - 1);
         uint32_t mo = (m + seg - 1) / seg;
         if (mo <= 1) break;
         m = mo;
     }
     return MBLS_SUCCESS;
+}
+
+// one (key, value) contribution: the histogram atomic's return value is the contribution's
+// rank inside its bucket, so the scatter needs no atomics (sorted[offsets[key] + rank]).
+// A wave whose lanes all hit one bucket (adversarial inputs: equal scalars) takes one atomic.
+MBLS_DEV void emit_digit(uint32_t key, uint32_t val, size_t o, uint32_t* __restrict__ keys,
+                         uint32_t* __restrict__ vals, uint32_t* __restrict__ ranks,
+                         uint32_t* __restrict__ counts) {
+    keys[o] = key;
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+    const uint64_t active = __ballot(1);
+    uint32_t rank = 0;
+    if (__ballot(key == k0) == active) {
+        if (k0 == INVALID_KEY) return;
+        const uint32_t leader = (uint32_t)__builtin_ctzll(active);
+        uint32_t base = 0;
+        if (__lane_id() == leader) base = atomicAdd(&counts[k0], (uint32_t)__popcll(active));
+        base = __shfl(base, leader, 64);
+        rank = base + (uint32_t)__popcll(active & ((1ull << __lane_id()) - 1));
+    } else if (key != INVALID_KEY) {
+        rank = atomicAdd(&counts[key], 1u);
+    }
+    if (key != INVALID_KEY) {
+        vals[o] = val;
+        ranks[o] = rank;
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -60,7 +96,7 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p) {
 template <bool MONT>
 __global__ __launch_bounds__(256) void k_digits(const uint8_t* __restrict__ scalars, uint32_t n, int c, int W, int Wg, uint32_t F,
                                                 uint32_t B, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                uint32_t* __restrict__ counts) {
+                                                uint32_t* __restrict__ ranks, uint32_t* __restrict__ counts) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
@@ -86,40 +122,364 @@ __global__ __launch_bounds__(256) void k_digits(const uint8_t* __restrict__ scal
             sign = 1;
             carry = 1;
         }
-        const size_t o = (size_t)w * n + i;
         const int f = w / Wg, wl = w % Wg;
         // precomputed bases are point-major: [P_i, 2^l P_i, ..., 2^((F-1) l) P_i] (core/msm.rs:164-165)
-        uint32_t key = INVALID_KEY;
-        if (v != 0) {
-            key = (uint32_t)wl * B + (v - 1);
-            vals[o] = ((i * F + (uint32_t)f) << 1) | sign;
-        }
-        keys[o] = key;
-        // histogram: one atomic per wave when the whole wave hits one bucket (adversarial
-        // inputs: equal scalars), else one per lane
-        const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
-        const uint64_t active = __ballot(1);
-        const uint64_t same = __ballot(key == k0);
-        if (same == active) {
-            if (k0 != INVALID_KEY && __lane_id() == (uint32_t)__builtin_ctzll(active))
-                atomicAdd(&counts[k0], (uint32_t)__popcll(active));
-        } else if (key != INVALID_KEY) {
-            atomicAdd(&counts[key], 1u);
-        }
+        emit_digit(v ? (uint32_t)wl * B + (v - 1) : INVALID_KEY, ((i * F + (uint32_t)f) << 1) | sign,
+                   (size_t)w * n + i, keys, vals, ranks, counts);
     }
     // canonical scalars (< r < 2^255) never leave a final carry: W*c >= 256 (checked for
     // c = 7..16 in tests/test_oracle.py)
 }
 
+// ------------------------------------------------------------------------------------
+// 1b. GLV digits (G1): s = +-m1 +- m2*lam (mod r), m1, m2 < 2^127 (oracle/pyref.py
+//     glv_decompose), lam = z^2 - 1 and r = lam^2 + lam + 1.  Point index i carries the m1
+//     digits, index n + i (the phi(P_i) table) the m2 digits; both halves share each window's
+//     buckets, so the windows halve (255 -> 127 bits) at the same contribution count.
+// ------------------------------------------------------------------------------------
+__constant__ uint32_t GLV_LAM[4] = {0xffffffffu, 0x00000000u, 0x0001a402u, 0xac45a401u};
+__constant__ uint32_t GLV_HALF[4] = {0x7fffffffu, 0x00000000u, 0x8000d201u, 0x5622d200u};
+// floor(2^383 / lam)
+__constant__ uint32_t GLV_G[8] = {0xc4b6396eu, 0xed2f27c6u, 0x9345fbd1u, 0x1c4fa4d3u,
+                                  0x7b67f718u, 0xb1fb7291u, 0xf00fd56eu, 0xbe35f678u};
+
+MBLS_DEV bool gt4(const uint32_t* a, const uint32_t* b) {  // a > b, 4 words
+    bool gt = false, eq = true;
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {
+        gt = gt || (eq && a[k] > b[k]);
+        eq = eq && a[k] == b[k];
+    }
+    return gt;
+}
+MBLS_DEV void sub4(uint32_t* d, const uint32_t* a, const uint32_t* b) {  // d = a - b
+    uint64_t br = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint64_t t = (uint64_t)a[k] - b[k] - br;
+        d[k] = (uint32_t)t;
+        br = (t >> 63) & 1;
+    }
+}
+MBLS_DEV void add4_u32(uint32_t* a, uint32_t x) {
+    uint64_t c = x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint64_t t = (uint64_t)a[k] + c;
+        a[k] = (uint32_t)t;
+        c = t >> 32;
+    }
+}
+MBLS_DEV void sub4_u32(uint32_t* a, uint32_t x) {
+    uint64_t br = x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint64_t t = (uint64_t)a[k] - br;
+        a[k] = (uint32_t)t;
+        br = (t >> 63) & 1;
+    }
+}
+
+MBLS_DEV void glv_split(const Fr& s, uint32_t (&m1)[4], bool& neg1, uint32_t (&m2)[4], bool& neg2) {
+    // q_est = floor(s * G / 2^383) in {q - 1, q}
+    uint32_t prod[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) prod[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint64_t t = (uint64_t)s.v[i] * GLV_G[j] + prod[i + j] + c;
+            prod[i + j] = (uint32_t)t;
+            c = t >> 32;
+        }
+        prod[i + 8] = (uint32_t)c;
+    }
+    uint32_t q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = (prod[11 + k] >> 31) | (prod[12 + k] << 1);
+    // rem = s - q * lam  (< 2 lam < 2^129)
+    uint32_t ql[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ql[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint64_t t = (uint64_t)q[i] * GLV_LAM[j] + ql[i + j] + c;
+            ql[i + j] = (uint32_t)t;
+            c = t >> 32;
+        }
+        ql[i + 4] = (uint32_t)c;
+    }
+    uint32_t rem[5];
+    {
+        uint64_t br = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint64_t t = (uint64_t)s.v[k] - ql[k] - br;
+            rem[k] = (uint32_t)t;
+            br = (t >> 63) & 1;
+        }
+    }
+    uint32_t k1[4] = {rem[0], rem[1], rem[2], rem[3]};
+    if (rem[4] != 0 || !gt4(GLV_LAM, k1)) {  // rem >= lam
+        sub4(k1, k1, GLV_LAM);
+        add4_u32(q, 1);
+    }
+    // balance k1 into (-lam/2, lam/2]
+    neg1 = gt4(k1, GLV_HALF);
+    if (neg1) {
+        sub4(m1, GLV_LAM, k1);
+        add4_u32(q, 1);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m1[k] = k1[k];
+    }
+    // balance k2: (k2 - lam - 1) * lam == k2 * lam + 1 (mod r), so k1 absorbs a -1
+    neg2 = gt4(q, GLV_HALF);
+    if (neg2) {
+        sub4(m2, GLV_LAM, q);
+        add4_u32(m2, 1);
+        if (neg1) {
+            add4_u32(m1, 1);
+        } else if ((m1[0] | m1[1] | m1[2] | m1[3]) == 0) {
+            m1[0] = 1;
+            neg1 = true;
+        } else {
+            sub4_u32(m1, 1);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m2[k] = q[k];
+    }
+}
+
+template <bool MONT>
+__global__ __launch_bounds__(256) void k_digits_glv(const uint8_t* __restrict__ scalars, uint32_t n, int c, int W,
+                                                    uint32_t B, uint32_t* __restrict__ keys,
+                                                    uint32_t* __restrict__ vals, uint32_t* __restrict__ ranks,
+                                                    uint32_t* __restrict__ counts) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
+    if (MONT) s = from_mont(s);
+    uint32_t m[2][4];
+    bool neg[2];
+    glv_split(s, m[0], neg[0], m[1], neg[1]);
+    const uint32_t mask = (1u << c) - 1;
+    const size_t stride = 2 * (size_t)n;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        uint32_t carry = 0;
+        for (int w = 0; w < W; ++w) {
+            const int bit = w * c;
+            const int word = bit >> 5, sh = bit & 31;
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                lo = (k == word) ? m[h][k] : lo;
+                hi = (k == word + 1) ? m[h][k] : hi;
+            }
+            uint64_t win = ((uint64_t)hi << 32) | lo;
+            uint32_t v = ((uint32_t)(win >> sh) & mask) + carry;
+            carry = 0;
+            uint32_t sign = neg[h] ? 1u : 0u;
+            if (v > B) {
+                v = (1u << c) - v;
+                sign ^= 1u;
+                carry = 1;
+            }
+            const uint32_t idx = (uint32_t)h * n + i;
+            emit_digit(v ? (uint32_t)w * B + (v - 1) : INVALID_KEY, (idx << 1) | sign, (size_t)w * stride + idx, keys,
+                       vals, ranks, counts);
+        }
+    }
+}
+
+// phi table: phi[i] = (beta x_i, y_i) (Montgomery); identity (0, 0) maps to itself.
+// beta: the cube root of unity in Fq with phi(G) = lam G (oracle/pyref.py GLV_BETA)
+__constant__ uint32_t GLV_BETA_MONT[12] = {0x8671f071u, 0xcd03c9e4u, 0x1fcda5d2u, 0x5dab2246u,
+                                           0xd3851b95u, 0x587042afu, 0x01bacb9eu, 0x8eb60ebeu,
+                                           0x83d050d2u, 0x03f97d6eu, 0x54638741u, 0x18f02065u};
+__global__ void k_glv_table(const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi, uint32_t n) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fq beta;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) beta.v[k] = GLV_BETA_MONT[k];
+    Affine<Fq> p = load_affine<Fq>(bases, i);
+    p.x = p.x * beta;
+    store_affine<Fq>(phi, i, p);
+}
+
+eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st) {
+    hipLaunchKernelGGL(k_glv_table, dim3((n + 255) / 256), dim3(256), 0, st, bases, phi, n);
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
+}
+
+// ------------------------------------------------------------------------------------
+// 1c. tiled digits (c <= 16): workgroup (tile, window) histograms its tile's digits in LDS
+//     (local rank = LDS atomic return), then flushes the histogram with ONE coalesced
+//     returning global add per bucket (base of this tile in the bucket).  Random-address
+//     global atomics run ~17x below the coalesced rate on CDNA4 (MI355X_MICROARCH.md, global
+//     atomics: "64 lanes in 64 different rows"); this is what k_digits paid per digit.
+//     Digit sources: NW words per index (GLV halves: 4 words, bit 127 = sign; plain: 8 words).
+// ------------------------------------------------------------------------------------
+static constexpr int DT_THREADS = 1024;
+static constexpr int DT_PER = 32;  // indices per thread
+static constexpr uint32_t DT_TILE = DT_THREADS * DT_PER;
+static constexpr uint32_t DT_MAX_B = 1u << 15;
+
+template <bool MONT>
+__global__ __launch_bounds__(256) void k_glv_split(const uint8_t* __restrict__ scalars, uint32_t n,
+                                                   uint4* __restrict__ out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
+    if (MONT) s = from_mont(s);
+    uint32_t m1[4], m2[4];
+    bool n1, n2;
+    glv_split(s, m1, n1, m2, n2);
+    out[i] = make_uint4(m1[0], m1[1], m1[2], m1[3] | (n1 ? 0x80000000u : 0u));
+    out[n + i] = make_uint4(m2[0], m2[1], m2[2], m2[3] | (n2 ? 0x80000000u : 0u));
+}
+
+__global__ void k_scalars_std(const uint8_t* __restrict__ scalars, uint32_t n, uint8_t* __restrict__ out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    store<FrCfg>(out + 32 * (size_t)i, from_mont(load<FrCfg>(scalars + 32 * (size_t)i)));
+}
+
+// signed digit of window w (carry chain from window 0), magnitude in v, sign in bit 31
+template <int NW>
+MBLS_DEV uint32_t digit_at(const uint32_t (&x)[NW], int w, int c, uint32_t B) {
+    const uint32_t mask = (1u << c) - 1;
+    uint32_t carry = 0, v = 0;
+    for (int j = 0; j <= w; ++j) {
+        const int bit = j * c;
+        const int word = bit >> 5, sh = bit & 31;
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            lo = (k == word) ? x[k] : lo;
+            hi = (k == word + 1) ? x[k] : hi;
+        }
+        v = ((uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & mask) + carry;
+        carry = v > B ? 1u : 0u;
+    }
+    return carry ? (((1u << c) - v) | 0x80000000u) : v;
+}
+
+// GLV: indices [0, 2n) over the split halves, vals (idx << 1 | sign), key w*B + v - 1.
+// plain: indices [0, n) over scalars, vals ((i*F + w/Wg) << 1 | sign), key (w%Wg)*B + v - 1.
+template <bool GLV>
+__global__ __launch_bounds__(DT_THREADS) void k_digits_tiled(const uint32_t* __restrict__ src, uint32_t nidx, int c,
+                                                             int Wg, uint32_t F, uint32_t B,
+                                                             uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                             uint32_t* __restrict__ ranks, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t hist[DT_MAX_B];
+    constexpr int NW = GLV ? 4 : 8;
+    const uint32_t tiles = (nidx + DT_TILE - 1) / DT_TILE;
+    const uint32_t tile = blockIdx.x % tiles;
+    const int w = (int)(blockIdx.x / tiles);
+    const uint32_t wl = GLV ? (uint32_t)w : (uint32_t)(w % Wg), f = GLV ? 0u : (uint32_t)(w / Wg);
+    for (uint32_t j = threadIdx.x; j < B; j += DT_THREADS) hist[j] = 0;
+    __syncthreads();
+    uint32_t dig[DT_PER], lr[DT_PER];
+#pragma unroll
+    for (int k = 0; k < DT_PER; ++k) {
+        const uint32_t idx = tile * DT_TILE + k * DT_THREADS + threadIdx.x;
+        dig[k] = 0;
+        lr[k] = 0;
+        if (idx < nidx) {
+            uint32_t x[NW];
+            const uint4* p = reinterpret_cast<const uint4*>(src) + (size_t)idx * (NW / 4);
+#pragma unroll
+            for (int q = 0; q < NW / 4; ++q) {
+                const uint4 u = p[q];
+                x[4 * q] = u.x;
+                x[4 * q + 1] = u.y;
+                x[4 * q + 2] = u.z;
+                x[4 * q + 3] = u.w;
+            }
+            uint32_t negh = 0;
+            if (GLV) {
+                negh = x[3] >> 31;
+                x[3] &= 0x7fffffffu;
+            }
+            const uint32_t d = digit_at<NW>(x, w, c, B) ^ (negh << 31);
+            dig[k] = d;
+            if (d & 0x7fffffffu) lr[k] = atomicAdd(&hist[(d & 0x7fffffffu) - 1], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < B; j += DT_THREADS) {
+        const uint32_t h = hist[j];
+        hist[j] = h ? atomicAdd(&counts[wl * B + j], h) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < DT_PER; ++k) {
+        const uint32_t idx = tile * DT_TILE + k * DT_THREADS + threadIdx.x;
+        if (idx >= nidx) continue;
+        const size_t o = (size_t)w * nidx + idx;
+        const uint32_t v = dig[k] & 0x7fffffffu, sign = dig[k] >> 31;
+        if (v == 0) {
+            keys[o] = INVALID_KEY;
+            continue;
+        }
+        keys[o] = wl * B + v - 1;
+        vals[o] = ((GLV ? idx : idx * F + f) << 1) | sign;
+        ranks[o] = hist[v - 1] + lr[k];
+    }
+}
+
+size_t digits_src_bytes(uint32_t n) { return (size_t)n * 32; }
+
 eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* keys,
-                           uint32_t* vals, uint32_t* counts, hipStream_t st) {
+                           uint32_t* vals, uint32_t* ranks, uint32_t* counts, uint8_t* dsrc, hipStream_t st) {
     dim3 g((n + 255) / 256);
-    if (mont)
+    if (P.B <= DT_MAX_B) {
+        const uint32_t* src;
+        uint32_t nidx;
+        if (P.glv) {
+            if (mont)
+                hipLaunchKernelGGL(k_glv_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+            else
+                hipLaunchKernelGGL(k_glv_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+            src = (const uint32_t*)dsrc;
+            nidx = 2 * n;
+        } else {
+            if (mont) hipLaunchKernelGGL(k_scalars_std, g, dim3(256), 0, st, scalars, n, dsrc);
+            src = (const uint32_t*)(mont ? dsrc : scalars);
+            nidx = n;
+        }
+        const uint32_t tiles = (nidx + DT_TILE - 1) / DT_TILE;
+        dim3 gt(tiles * (uint32_t)P.W);
+        if (P.glv)
+            hipLaunchKernelGGL(k_digits_tiled<true>, gt, dim3(DT_THREADS), 0, st, src, nidx, P.c, P.Wg, (uint32_t)P.F,
+                               P.B, keys, vals, ranks, counts);
+        else
+            hipLaunchKernelGGL(k_digits_tiled<false>, gt, dim3(DT_THREADS), 0, st, src, nidx, P.c, P.Wg,
+                               (uint32_t)P.F, P.B, keys, vals, ranks, counts);
+        MBLS_TRY(hipGetLastError());
+        return MBLS_SUCCESS;
+    }
+    if (P.glv) {
+        if (mont)
+            hipLaunchKernelGGL(k_digits_glv<true>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.B, keys, vals, ranks, counts);
+        else
+            hipLaunchKernelGGL(k_digits_glv<false>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.B, keys, vals, ranks, counts);
+    } else if (mont)
         hipLaunchKernelGGL(k_digits<true>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, (uint32_t)P.F, P.B, keys,
-                           vals, counts);
+                           vals, ranks, counts);
     else
         hipLaunchKernelGGL(k_digits<false>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, (uint32_t)P.F, P.B, keys,
-                           vals, counts);
+                           vals, ranks, counts);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }
@@ -232,32 +592,19 @@ eIcicleError launch_chunk_counts(const uint32_t* counts, uint32_t* nchunks, uint
 // 3. scatter (counting sort)
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                                 size_t total, uint32_t* __restrict__ cursor, uint32_t* __restrict__ sorted) {
+                                                 const uint32_t* __restrict__ ranks, size_t total,
+                                                 const uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= total) return;
     const uint32_t k = keys[i];
-    // wave-uniform bucket (adversarial inputs): one atomic reserves the wave's slots
-    const uint32_t k0 = __builtin_amdgcn_readfirstlane(k);
-    const uint64_t active = __ballot(1);
-    if (__ballot(k == k0) == active) {
-        if (k0 == INVALID_KEY) return;
-        uint32_t base = 0;
-        const uint32_t leader = (uint32_t)__builtin_ctzll(active);
-        if (__lane_id() == leader) base = atomicAdd(&cursor[k0], (uint32_t)__popcll(active));
-        base = __shfl(base, leader, 64);
-        const uint32_t rank = (uint32_t)__popcll(active & ((1ull << __lane_id()) - 1));
-        sorted[base + rank] = vals[i];
-        return;
-    }
     if (k == INVALID_KEY) return;
-    uint32_t pos = atomicAdd(&cursor[k], 1u);
-    sorted[pos] = vals[i];
+    sorted[offsets[k] + ranks[i]] = vals[i];
 }
 
-eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, size_t total, uint32_t* cursor,
-                            uint32_t* sorted, hipStream_t st) {
-    hipLaunchKernelGGL(k_scatter, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, keys, vals, total, cursor,
-                       sorted);
+eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const uint32_t* ranks, size_t total,
+                            const uint32_t* offsets, uint32_t* sorted, hipStream_t st) {
+    hipLaunchKernelGGL(k_scatter, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, keys, vals, ranks, total,
+                       offsets, sorted);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }

@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "mbls_common.hpp"
@@ -37,33 +39,42 @@ namespace mbls {
 
 static constexpr uint32_t INVALID_KEY = 0xffffffffu;
 static constexpr int CHUNK = 16;  // max points per accumulation thread
-static constexpr int SEG = 16;    // inputs per reduction segment, levels >= 1 (row-sliced)
-static constexpr int SEG_LOG = 4;
-static constexpr int SEG0 = 4;    // level 0 (one segment per lane): short chains, many lanes
-static constexpr int SEG0_LOG = 2;
+static constexpr int SEG_LOG = 4;   // default segment length 16, levels >= 1 (row-sliced)
+static constexpr int SEG0_LOG = 2;  // level 0 (one segment per lane): short chains, many lanes
 static constexpr int MAX_MSM_LOG = 26;
 static constexpr int SCAN_BLOCK = 1024;
-static constexpr int MAX_LEVELS = 8;
+static constexpr int MAX_LEVELS = 16;
 
 struct MsmPlan {
     int c, W, Wg, F;
+    bool glv;                   // G1 endomorphism split (msm_common.hip k_digits_glv)
     uint32_t B, TB;
+    size_t pts;                 // distinct point indices (n, n*F, or 2n with GLV)
     size_t contributions;
     int levels;                 // bucket-reduction levels
     uint32_t level_m[MAX_LEVELS];  // inputs per window at each level
+    uint8_t seg_log[MAX_LEVELS];   // log2 segment length per level
+    uint32_t seg(int l) const { return 1u << seg_log[l]; }
+    uint64_t seg_logs_packed() const {  // 4 bits per level, for k_window_horner
+        uint64_t v = 0;
+        for (int l = 0; l < levels; ++l) v |= (uint64_t)seg_log[l] << (4 * l);
+        return v;
+    }
 };
 
-eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p);
+eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, bool allow_glv = false);
 
 // ---- non-templated launchers (msm_common.hip) ----------------------------------------
 eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* keys,
-                           uint32_t* vals, uint32_t* counts, hipStream_t st);
+                           uint32_t* vals, uint32_t* ranks, uint32_t* counts, uint8_t* dsrc, hipStream_t st);
+size_t digits_src_bytes(uint32_t n);
 eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint32_t* tmp, hipStream_t st);
 eIcicleError launch_chunk_counts(const uint32_t* counts, uint32_t* nchunks, uint32_t m, hipStream_t st);
-eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, size_t total, uint32_t* cursor,
-                            uint32_t* sorted, hipStream_t st);
+eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const uint32_t* ranks, size_t total,
+                            const uint32_t* offsets, uint32_t* sorted, hipStream_t st);
 eIcicleError launch_chunk_owner(const uint32_t* chunk_off, uint32_t m, uint32_t* owner, hipStream_t st);
 eIcicleError launch_scalars_from_mont(uint8_t* s, size_t n, hipStream_t st);
+eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
 size_t scan_tmp_words(uint32_t m);
 
 // ------------------------------------------------------------------------------------
@@ -73,7 +84,8 @@ template <class F>
 __global__ __launch_bounds__(256) void k_accumulate(const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ chunk_off,
                                                     const uint32_t* __restrict__ owner, uint32_t TB, uint32_t max_chunks,
-                                                    const uint8_t* __restrict__ bases, uint8_t* __restrict__ partials) {
+                                                    const uint8_t* __restrict__ bases, const uint8_t* __restrict__ phi,
+                                                    uint32_t nsplit, uint8_t* __restrict__ partials) {
     uint32_t ch = blockIdx.x * blockDim.x + threadIdx.x;
     if (ch >= max_chunks || ch >= chunk_off[TB]) return;
     uint32_t b = owner[ch];
@@ -81,11 +93,22 @@ __global__ __launch_bounds__(256) void k_accumulate(const uint32_t* __restrict__
     uint32_t beg = offsets[b] + k * CHUNK;
     uint32_t end = min(beg + CHUNK, offsets[b + 1]);
     Jacobian<F> acc = Jacobian<F>::inf();
+    // GLV: indices >= nsplit address the phi(P) table
+    auto fetch = [&](uint32_t v) {
+        uint32_t idx = v >> 1;
+        const uint8_t* src = idx >= nsplit ? phi : bases;
+        idx = idx >= nsplit ? idx - nsplit : idx;
+        return load_affine<F>(src, idx);
+    };
+    // one point ahead: the next random 96/192-byte fetch overlaps this mixed addition
+    uint32_t v = sorted[beg];
+    Affine<F> p = fetch(v);
     for (uint32_t e = beg; e < end; ++e) {
-        uint32_t v = sorted[e];
-        Affine<F> p = load_affine<F>(bases, v >> 1);
-        if (v & 1) p = aff_neg(p);
-        acc = jac_madd(acc, p);
+        const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
+        const Affine<F> pn = fetch(vn);
+        acc = jac_madd(acc, (v & 1) ? aff_neg(p) : p);
+        v = vn;
+        p = pn;
     }
     store_jac<F>(partials, ch, acc);
 }
@@ -96,38 +119,41 @@ __global__ __launch_bounds__(256) void k_accumulate(const uint32_t* __restrict__
 //    log passes instead of one serial thread.  Passes past the largest bucket exit at once
 //    (maxc = max chunks per bucket, computed on device).
 // ------------------------------------------------------------------------------------
-static constexpr int TREE_FANIN = 4;
+static constexpr int TREE_FANIN = 8;
+static constexpr int SMALL_MAX = 16;  // buckets of <= SMALL_MAX chunks: one thread (k_bucket_small)
 
 template <class F>
 __global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict__ chunk_off,
                                                      const uint32_t* __restrict__ owner, uint32_t TB,
                                                      uint32_t max_chunks, const uint32_t* __restrict__ maxc,
                                                      uint32_t step, uint8_t* __restrict__ partials) {
-    if (*maxc <= TREE_FANIN || step >= *maxc) return;  // only heavy buckets remain
-    uint32_t ch = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ch >= max_chunks || ch >= chunk_off[TB]) return;
-    const uint32_t b = owner[ch];
-    const uint32_t j = ch - chunk_off[b];
-    const uint32_t cnt = chunk_off[b + 1] - chunk_off[b];
-    if (cnt <= TREE_FANIN) return;  // summed by k_bucket_small
-    if (j % (TREE_FANIN * step) != 0 || j + step >= cnt) return;
-    Jacobian<F> acc = load_jac<F>(partials, ch);
-    for (int g = 1; g < TREE_FANIN; ++g) {
-        uint32_t o = j + g * step;
-        if (o >= cnt) break;
-        acc = jac_add(acc, load_jac<F>(partials, (size_t)ch + g * step));
+    if (*maxc <= SMALL_MAX || step >= *maxc) return;  // only heavy buckets remain
+    const uint32_t total = min(max_chunks, chunk_off[TB]);
+    // capped grid, grid-stride: a pass that finds no work costs one small launch
+    for (uint32_t ch = blockIdx.x * blockDim.x + threadIdx.x; ch < total; ch += gridDim.x * blockDim.x) {
+        const uint32_t b = owner[ch];
+        const uint32_t j = ch - chunk_off[b];
+        const uint32_t cnt = chunk_off[b + 1] - chunk_off[b];
+        if (cnt <= SMALL_MAX) continue;  // summed by k_bucket_small
+        if (j % (TREE_FANIN * step) != 0 || j + step >= cnt) continue;
+        Jacobian<F> acc = load_jac<F>(partials, ch);
+        for (int g = 1; g < TREE_FANIN; ++g) {
+            uint32_t o = j + g * step;
+            if (o >= cnt) break;
+            acc = jac_add(acc, load_jac<F>(partials, (size_t)ch + g * step));
+        }
+        store_jac<F>(partials, ch, acc);
     }
-    store_jac<F>(partials, ch, acc);
 }
 
-// common case: one thread per bucket sums its <= TREE_FANIN chunk partials (all lanes busy)
+// common case: one thread per bucket sums its <= SMALL_MAX chunk partials
 template <class F>
 __global__ __launch_bounds__(256) void k_bucket_small(const uint32_t* __restrict__ chunk_off, uint32_t m,
                                                       const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
     const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
-    if (k1 - k0 > TREE_FANIN) return;  // heavy: tree passes + k_bucket_gather
+    if (k1 - k0 > SMALL_MAX) return;  // heavy: tree passes + k_bucket_gather
     Jacobian<F> acc = Jacobian<F>::inf();
     if (k1 > k0) acc = load_jac<F>(partials, k0);
     for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<F>(partials, k));
@@ -138,11 +164,11 @@ template <class F>
 __global__ __launch_bounds__(256) void k_bucket_gather(const uint32_t* __restrict__ chunk_off, uint32_t m,
                                                        const uint32_t* __restrict__ maxc,
                                                        const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
-    if (*maxc <= TREE_FANIN) return;
+    if (*maxc <= SMALL_MAX) return;
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
     const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
-    if (k1 - k0 > TREE_FANIN) store_jac<F>(buckets, b, load_jac<F>(partials, k0));
+    if (k1 - k0 > SMALL_MAX) store_jac<F>(buckets, b, load_jac<F>(partials, k0));
 }
 
 // ------------------------------------------------------------------------------------
@@ -255,15 +281,15 @@ __global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V,
     if (r == 0) rstore_jac<F>(out, blockIdx.x, acc);
 }
 
-// G_w = sumT[0] + seg0*(sumT[1] + SEG*(sumT[2] + ...)): sums[l * Wg + w]; one row per window
+// G_w = sumT[0] + seg_0*(sumT[1] + seg_1*(sumT[2] + ...)): sums[l * Wg + w]; one row per window
 template <class F>
-__global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, int Wg, int seg0_log,
+__global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, int Wg, uint64_t seg_logs,
                                 uint8_t* __restrict__ windows) {
     const int w = (int)row_id();
     if (w >= Wg) return;
     RJac<F> acc = rload_jac<F>(sums, (size_t)(levels - 1) * Wg + w);
     for (int l = levels - 2; l >= 0; --l) {
-        const int dbls = (l == 0) ? seg0_log : SEG_LOG;
+        const int dbls = (int)((seg_logs >> (4 * l)) & 15);
         for (int k = 0; k < dbls; ++k) acc = jac_dbl(acc);
         acc = jac_add(acc, rload_jac<F>(sums, (size_t)l * Wg + w));
     }
@@ -432,21 +458,23 @@ struct GroupTraits<Fq2> {
 };
 
 struct MsmScratchSizes {
-    size_t keys, vals, sorted, words, tmp, owner, partials, buckets, levelT, levelR, sums, windows, treetmp;
+    size_t dsrc, keys, vals, ranks, sorted, words, tmp, owner, partials, buckets, levelT, levelR, sums, windows, treetmp, phi;
     size_t total() const {
-        return keys + vals + sorted + 5 * words + tmp + owner + partials + buckets + levelT + levelR + sums + windows +
-               2 * treetmp;
+        return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + partials + buckets + levelT + levelR + sums + windows +
+               2 * treetmp + phi;
     }
 };
 
-inline uint32_t level_seg(int l) { return l == 0 ? SEG0 : SEG; }
 inline uint32_t tree_blocks(uint32_t m) { return (m + 16 * TREE_PER_ROW - 1) / (16 * TREE_PER_ROW); }
 
-inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, uint32_t max_chunks) {
+inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks) {
     MsmScratchSizes z;
+    z.phi = P.glv ? align_up(P.pts / 2 * aff) : 0;
     const size_t NC = P.contributions;
     z.keys = align_up(NC * 4);
     z.vals = align_up(NC * 4);
+    z.ranks = align_up(NC * 4);
+    z.dsrc = align_up(digits_src_bytes((uint32_t)(P.glv ? P.pts / 2 : P.pts / P.F)));
     z.sorted = align_up(NC * 4);
     z.words = align_up(((size_t)P.TB + 1) * 4);
     z.tmp = align_up(scan_tmp_words(max_chunks > P.TB ? max_chunks : P.TB) * 4);
@@ -455,7 +483,7 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, uint32_t 
     z.buckets = align_up((size_t)P.TB * jac);
     size_t lv = 0, maxblk = 1;
     for (int l = 0; l < P.levels; ++l) {
-        uint32_t mo = (P.level_m[l] + level_seg(l) - 1) / level_seg(l);
+        uint32_t mo = (P.level_m[l] + P.seg(l) - 1) / P.seg(l);
         lv += mo;
         maxblk = maxblk > tree_blocks(mo) ? maxblk : tree_blocks(mo);
     }
@@ -471,8 +499,9 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, uint32_t 
 // (F*n entries when precomputed); result: one Jacobian Montgomery point on device.
 template <class F>
 eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t* bases, uint32_t n,
-                        const MsmPlan& P, uint8_t* result, Arena& arena, hipStream_t st) {
-    constexpr size_t JAC = GroupTraits<F>::JAC;
+                        const MsmPlan& P, uint8_t* result, StreamCtx& ctx, hipStream_t st) {
+    Arena& arena = ctx.arena;
+    constexpr size_t JAC = GroupTraits<F>::JAC, AFF = GroupTraits<F>::AFF;
     if (n == 0) {
         hipLaunchKernelGGL(k_store_inf<F>, dim3(1), dim3(64), 0, st, result, 1);
         MBLS_TRY(hipGetLastError());
@@ -481,13 +510,14 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     const uint32_t TB = P.TB;
     const size_t NC = P.contributions;
     const uint32_t max_chunks = (uint32_t)(NC / CHUNK + TB + 1);
-    MsmScratchSizes z = msm_scratch_sizes(P, JAC, max_chunks);
+    MsmScratchSizes z = msm_scratch_sizes(P, JAC, AFF, max_chunks);
     uint32_t* keys = (uint32_t*)arena.take(z.keys);
     uint32_t* vals = (uint32_t*)arena.take(z.vals);
+    uint32_t* ranks = (uint32_t*)arena.take(z.ranks);
+    uint8_t* dsrc = (uint8_t*)arena.take(z.dsrc);
     uint32_t* sorted = (uint32_t*)arena.take(z.sorted);
     uint32_t* counts = (uint32_t*)arena.take(z.words);
     uint32_t* offsets = (uint32_t*)arena.take(z.words);
-    uint32_t* cursor = (uint32_t*)arena.take(z.words);
     uint32_t* nchunks = (uint32_t*)arena.take(z.words);
     uint32_t* chunk_off = (uint32_t*)arena.take(z.words);
     uint32_t* tmp = (uint32_t*)arena.take(z.tmp);
@@ -500,52 +530,58 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint8_t* windows = (uint8_t*)arena.take(z.windows);
     uint8_t* tree_a = (uint8_t*)arena.take(z.treetmp);
     uint8_t* tree_b = (uint8_t*)arena.take(z.treetmp);
-    if (!tree_b) return MBLS_ALLOCATION_FAILED;
+    uint8_t* phi = P.glv ? (uint8_t*)arena.take(z.phi) : nullptr;
+    if (!tree_b || (P.glv && !phi)) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
     {
         ProfScope ps("msm.digits", st);
         MBLS_TRY(hipMemsetAsync(counts, 0, (size_t)TB * 4, st));
-        er = launch_digits(scalars, scalars_mont, n, P, keys, vals, counts, st);
+        er = launch_digits(scalars, scalars_mont, n, P, keys, vals, ranks, counts, dsrc, st);
         if (er != MBLS_SUCCESS) return er;
+        if (P.glv && (er = launch_glv_table(bases, phi, n, st)) != MBLS_SUCCESS) return er;
     }
     {
         ProfScope ps("msm.sort", st);
         if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) return er;
-        MBLS_TRY(hipMemcpyAsync(cursor, offsets, (size_t)TB * 4, hipMemcpyDeviceToDevice, st));
         if ((er = launch_chunk_counts(counts, nchunks, TB, st)) != MBLS_SUCCESS) return er;
         if ((er = scan_exclusive(nchunks, chunk_off, TB, tmp, st)) != MBLS_SUCCESS) return er;
-        if ((er = launch_scatter(keys, vals, NC, cursor, sorted, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
         if ((er = launch_chunk_owner(chunk_off, TB, owner, st)) != MBLS_SUCCESS) return er;
     }
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
         ProfScope ps("msm.accumulate", st);
+        // 222 VGPRs -> 2 waves/SIMD; forcing 3 spills 228 B/lane and runs 17% slower (measured)
         hipLaunchKernelGGL(k_accumulate<F>, dim3((max_chunks + 255) / 256), dim3(256), 0, st, sorted, offsets,
-                           chunk_off, owner, TB, max_chunks, bases, partials);
+                           chunk_off, owner, TB, max_chunks, bases, phi, P.glv ? n : 0xffffffffu, partials);
     }
     {
         ProfScope ps("msm.bucket_sum", st);
         // worst case: every contribution of a window group in one bucket
-        const uint32_t max_per_bucket = (uint32_t)(((size_t)n * P.F + CHUNK - 1) / CHUNK);
+        const uint32_t max_per_bucket = (uint32_t)((P.pts + CHUNK - 1) / CHUNK);
         hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials,
                            buckets);
-        if (max_per_bucket > TREE_FANIN) {
+        if (max_per_bucket > SMALL_MAX) {
             for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
-                hipLaunchKernelGGL(k_bucket_tree<F>, dim3((max_chunks + 255) / 256), dim3(256), 0, st, chunk_off,
+                hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks + 255) / 256, 1024u)), dim3(256), 0, st, chunk_off,
                                    owner, TB, max_chunks, nchunks + TB, step, partials);
             hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB,
                                nchunks + TB, partials, buckets);
         }
     }
     ProfScope ps_red("msm.reduce", st);
-    // recursive running-sum reduction
+    // recursive running-sum reduction.  The per-level T tree sums are latency-bound chains off
+    // the critical path: they run on the context's side stream, forked after each level and
+    // joined before the window Horner.
+    if ((er = ctx.ensure_side((size_t)P.levels + 1)) != MBLS_SUCCESS) return er;
+    hipStream_t side = ctx.side;
     const uint8_t* V = buckets;
     size_t lvoff = 0;
     for (int l = 0; l < P.levels; ++l) {
         const uint32_t m_in = P.level_m[l];
-        const uint32_t seg = level_seg(l);
+        const uint32_t seg = P.seg(l);
         const uint32_t m_out = (m_in + seg - 1) / seg;
         uint8_t* T = levelT + lvoff * JAC;
         uint8_t* R = levelR + lvoff * JAC;
@@ -559,6 +595,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
                                P.Wg, 0, T, R);
         }
         // sum of this level's T per window: tree stages until one point per window
+        MBLS_TRY(hipEventRecord(ctx.events[l], st));
+        MBLS_TRY(hipStreamWaitEvent(side, ctx.events[l], 0));
         const uint8_t* src = T;
         uint32_t m = m_out;
         uint8_t* pp[2] = {tree_a, tree_b};
@@ -566,7 +604,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         while (true) {
             const uint32_t nblk = tree_blocks(m);
             uint8_t* dst = (nblk == 1) ? sums + (size_t)l * P.Wg * JAC : pp[flip];
-            hipLaunchKernelGGL(k_tree_sum<F>, dim3(P.Wg * nblk), dim3(256), 0, st, src, m, nblk, dst);
+            hipLaunchKernelGGL(k_tree_sum<F>, dim3(P.Wg * nblk), dim3(256), 0, side, src, m, nblk, dst);
             if (nblk == 1) break;
             src = dst;
             m = nblk;
@@ -575,7 +613,9 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         V = R;
         lvoff += (size_t)m_out * P.Wg;
     }
-    hipLaunchKernelGGL(k_window_horner<F>, dim3((P.Wg * 16 + 63) / 64), dim3(64), 0, st, sums, P.levels, P.Wg, SEG0_LOG,
+    MBLS_TRY(hipEventRecord(ctx.events[P.levels], side));
+    MBLS_TRY(hipStreamWaitEvent(st, ctx.events[P.levels], 0));
+    hipLaunchKernelGGL(k_window_horner<F>, dim3((P.Wg * 16 + 63) / 64), dim3(64), 0, st, sums, P.levels, P.Wg, P.seg_logs_packed(),
                        windows);
     {
         ProfScope ps("msm.final", st);
@@ -598,7 +638,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     hipStream_t st = static_cast<hipStream_t>(cfg->stream);
     const int batch = icicle_semantics ? (cfg->batch_size > 0 ? cfg->batch_size : 1) : 1;
     MsmPlan P;
-    eIcicleError er = make_plan(msm_size > 0 ? msm_size : 1, cfg, P);
+    eIcicleError er = make_plan(msm_size > 0 ? msm_size : 1, cfg, P, std::is_same<F, Fq>::value);
     if (er != MBLS_SUCCESS) return er;
     const bool scal_mont = icicle_semantics ? cfg->are_scalars_montgomery_form : false;
     const bool pts_mont = icicle_semantics ? cfg->are_points_montgomery_form : true;
@@ -615,7 +655,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     size_t st_b = (!cfg->are_points_on_device || !pts_mont) ? align_up(nbases * AFF) : 0;
     size_t st_r = align_up(JAC * (size_t)batch);
     uint32_t max_chunks = (uint32_t)(P.contributions / CHUNK + P.TB + 1);
-    size_t scratch = msm_scratch_sizes(P, JAC, max_chunks).total();
+    size_t scratch = msm_scratch_sizes(P, JAC, AFF, max_chunks).total();
     er = A.reserve(st_s + st_b + st_r + scratch + 4096);
     if (er != MBLS_SUCCESS) return er;
 
@@ -643,7 +683,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
         A.rewind(mark);  // scratch reused across the batch (stream-ordered)
         const uint8_t* sb = d_s + (size_t)b * n * 32;
         const uint8_t* bb = d_b + (shared ? 0 : (size_t)b * nbases_per * AFF);
-        er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, A, st);
+        er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, ctx, st);
         if (er != MBLS_SUCCESS) return er;
     }
     if (icicle_semantics) {

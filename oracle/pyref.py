@@ -316,6 +316,42 @@ def signed_digits(s: int, c: int, num_windows: int):
     return out, carry
 
 
+# --------------------------------------------------------------------------------------
+# GLV split used by the G1 MSM kernel (k_digits_glv).  Not a reference algorithm: the
+# reference ships GLV constants only behind an experimental flag, off the MSM path
+# (bls12-381/src/curve/point_ops.cu:103-145); the MSM result is unchanged by the split.
+# r = lam^2 + lam + 1 exactly (lam = z^2 - 1), phi(x, y) = (beta x, y) = lam * P on G1.
+# --------------------------------------------------------------------------------------
+BLS_Z = -0xD201000000010000
+GLV_LAMBDA = BLS_Z * BLS_Z - 1
+GLV_BETA = 0x1A0111EA397FE699EC02408663D4DE85AA0D857D89759AD4897D29650FB85F9B409427EB4F49FFFD8BFD00000000AAAC
+
+
+def glv_phi(pt):
+    return None if pt is None else (GLV_BETA * pt[0] % P, pt[1])
+
+
+def glv_decompose(s: int):
+    """(m1, neg1, m2, neg2) with s == (+-m1) + (+-m2) * lam (mod r) and m1, m2 < 2^127,
+    following the kernel step by step: q = floor(s / lam), balance k1 then k2."""
+    lam = GLV_LAMBDA
+    q, k1 = divmod(s, lam)
+    half = lam >> 1
+    m1, neg1, k2 = k1, False, q
+    if k1 > half:
+        m1, neg1, k2 = lam - k1, True, q + 1
+    m2, neg2 = k2, False
+    if k2 > half:
+        m2, neg2 = lam + 1 - k2, True   # (k2 - lam - 1) * lam == k2 * lam + 1 (mod r)
+        if neg1:
+            m1 += 1
+        elif m1 == 0:
+            m1, neg1 = 1, True
+        else:
+            m1 -= 1
+    return m1, neg1, m2, neg2
+
+
 def rng(seed: int) -> random.Random:
     return random.Random(seed)
 

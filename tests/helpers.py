@@ -142,3 +142,12 @@ def oracle_ntt(data_mont: np.ndarray, log_n: int, inverse: bool, threads=0):
     a = np.ascontiguousarray(data_mont.copy())
     oracle().orc_ntt(ptr(a), log_n, 1 if inverse else 0, threads)
     return a
+
+
+def glv_edge_scalars():
+    """scalars on the GLV split's balancing boundaries (k1, k2 around lam/2, lam, lam + 1)"""
+    lam, h = pyref.GLV_LAMBDA, pyref.GLV_LAMBDA >> 1
+    out = [0, 1, 2, pyref.R - 1, pyref.R - 2, h, h + 1, lam - 1, lam, lam + 1, lam * lam, lam * lam + lam,
+           (h + 1) * lam, h * lam + h, h * lam + h + 1, (h + 1) * lam + h + 1, (h + 2) * lam - 1, (lam + 1) * lam - 1,
+           lam * lam + lam - 1, (1 << 254), (1 << 255) - 1]
+    return [s % pyref.R for s in out]

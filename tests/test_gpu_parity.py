@@ -307,3 +307,25 @@ def test_msm_sum_jacobian_and_convert(amd, gh):
     amd.jacobian_to_icicle("g1", tot)
     torch.cuda.synchronize()
     assert gh.decode_icicle("g1", amd.to_numpy_u64(tot)[0]) == H.pt_from_json(case["result"], "g1")
+
+
+def test_msm_glv_split_boundaries(amd, gh):
+    """G1 runs the GLV split (phi(P) = lam P, half-width digits): scalars on its balancing
+    boundaries, full-width and <= 128-bit (bitsize 128 keeps the plain path) against the oracle"""
+    import torch
+    edge = H.glv_edge_scalars()
+    g = pr.rng(21)
+    sc = edge + [g.randrange(pr.R) for _ in range(64 - len(edge))]
+    n = len(sc)
+    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 77)
+    bn = amd.to_numpy_u64(b)
+    s = H.ints_to_limbs(sc, 4)
+    ref = H.g1_from_affine_mont(H.oracle_msm("g1", s, bn))
+    for c in (0, 4, 9, 16):
+        r = amd.msm("g1", s, bn, c=c, n=n)
+        assert gh.decode_icicle("g1", r[0]) == ref, c
+    small = H.ints_to_limbs([x % (1 << 128) for x in sc], 4)
+    ref = H.g1_from_affine_mont(H.oracle_msm("g1", small, bn))
+    r = amd.msm("g1", small, bn, bitsize=128, n=n)
+    assert gh.decode_icicle("g1", r[0]) == ref
