@@ -194,6 +194,12 @@ eIcicleError scalar_mul_vec_cuda(mbls_fr_t* output, const mbls_fr_t* scalar, con
                                  const VecOpsConfig* config);
 eIcicleError scalar_add_vec_cuda(mbls_fr_t* output, const mbls_fr_t* scalar, const mbls_fr_t* vec, int size,
                                  const VecOpsConfig* config);
+/* sum of `size` device elements; output on device or host per config->is_result_on_device.
+ * Replaces vec_sum_cuda (vec_ops.cu:479-524; the reference takes `const VecOpsConfig&`). */
+eIcicleError vec_sum_cuda(mbls_fr_t* output, const mbls_fr_t* input, int size, const VecOpsConfig* config);
+/* element-wise inverses (0 -> 0), device pointers, in place allowed.  Replaces the C++
+ * template vec_ops::batch_inv_cuda<Fr> (vec_ops.cu:606-673); a C symbol here. */
+eIcicleError bls12_381_batch_inv_cuda(mbls_fr_t* output, const mbls_fr_t* input, int size, const VecOpsConfig* config);
 
 /* ------------------------------------------------------------------------------------ */
 /* library utilities (no reference counterpart; used by the host API, tests and bench)   */

@@ -67,7 +67,7 @@ EXPORTED = [
     "bls12_381_field_ntt_release_domain_cuda",
     "bls12_381_vector_add", "bls12_381_vector_sub", "bls12_381_vector_mul", "bls12_381_scalar_mul_vec",
     "bls12_381_scalar_add_vec", "vec_add_cuda", "vec_sub_cuda", "vec_mul_cuda", "scalar_mul_vec_cuda",
-    "scalar_add_vec_cuda",
+    "scalar_add_vec_cuda", "vec_sum_cuda", "bls12_381_batch_inv_cuda",
     "mbls_version", "mbls_error_string", "mbls_gen_scalars", "mbls_gen_g1_bases", "mbls_gen_g2_bases",
     "mbls_g1_sum_jacobian", "mbls_g2_sum_jacobian", "mbls_g1_jacobian_to_icicle", "mbls_g2_jacobian_to_icicle",
     "mbls_profile_enable", "mbls_profile_reset", "mbls_profile_read",
@@ -100,6 +100,7 @@ def lib():
         "bls12_381_scalar_add_vec": [P, P, sz, P, P],
         "vec_add_cuda": [P, P, P, i32, P], "vec_sub_cuda": [P, P, P, i32, P], "vec_mul_cuda": [P, P, P, i32, P],
         "scalar_mul_vec_cuda": [P, P, P, i32, P], "scalar_add_vec_cuda": [P, P, P, i32, P],
+        "vec_sum_cuda": [P, P, i32, P], "bls12_381_batch_inv_cuda": [P, P, i32, P],
         "mbls_gen_scalars": [P, u64, sz, b, P], "mbls_gen_g1_bases": [P, u64, sz, P],
         "mbls_gen_g2_bases": [P, u64, sz, P], "mbls_g1_sum_jacobian": [P, i32, P, P],
         "mbls_g2_sum_jacobian": [P, i32, P, P], "mbls_g1_jacobian_to_icicle": [P, i32, P],
@@ -207,15 +208,31 @@ _VEC = {"add": "bls12_381_vector_add", "sub": "bls12_381_vector_sub", "mul": "bl
         "scalar_mul": "bls12_381_scalar_mul_vec", "scalar_add": "bls12_381_scalar_add_vec"}
 
 
-def vec_op(op, a, b, out=None, stream=None, is_async=False):
-    """a, b: (n,4) uint64 numpy (host) or torch (device) arrays; for scalar ops `a` is one
-    element (host numpy (4,) unless it is a device tensor)."""
-    n = b.shape[0]
+def vec_op(op, a, b, out=None, stream=None, is_async=False, batch=1, columns_batch=False):
+    """a, b: (batch*n,4) uint64 numpy (host) or torch (device) arrays; for scalar ops `a`
+    holds one element per batch member (host numpy unless it is a device tensor)."""
+    total = b.shape[0]
     if out is None:
-        out = np.zeros((n, 4), dtype=np.uint64)
+        out = np.zeros((total, 4), dtype=np.uint64)
     cfg = vec_config(is_a_on_device=_is_dev(a), is_b_on_device=_is_dev(b), is_result_on_device=_is_dev(out),
-                     is_async=is_async, stream=stream)
-    check(getattr(lib(), _VEC[op])(_p(a), _p(b), n, ctypes.byref(cfg), _p(out)), _VEC[op])
+                     is_async=is_async, stream=stream, batch_size=batch, columns_batch=columns_batch)
+    check(getattr(lib(), _VEC[op])(_p(a), _p(b), total // batch, ctypes.byref(cfg), _p(out)), _VEC[op])
+    return out
+
+
+def vec_sum(x, out=None, stream=None):
+    """sum of the device tensor x (n,4) -> (1,4) numpy (host) unless `out` is a device tensor"""
+    if out is None:
+        out = np.zeros((1, 4), dtype=np.uint64)
+    cfg = vec_config(is_a_on_device=True, is_b_on_device=True, is_result_on_device=_is_dev(out), stream=stream)
+    check(lib().vec_sum_cuda(_p(out), _p(x), x.shape[0], ctypes.byref(cfg)), "vec_sum_cuda")
+    return out
+
+
+def batch_inv(x, out, stream=None):
+    """element-wise inverses of device tensor x into device tensor out (may be x)"""
+    cfg = vec_config(stream=stream)
+    check(lib().bls12_381_batch_inv_cuda(_p(out), _p(x), x.shape[0], ctypes.byref(cfg)), "bls12_381_batch_inv_cuda")
     return out
 
 
@@ -229,14 +246,18 @@ def ntt_init_domain(root_mont=None):
                                                ctypes.byref(cfg)), "ntt_init_domain")
 
 
-def ntt(x, inverse=False, out=None, batch=1, stream=None, is_async=False, coset_gen=None):
+ORDERINGS = {"NN": 0, "NR": 1, "RN": 2, "RR": 3, "NM": 4, "MN": 5}
+
+
+def ntt(x, inverse=False, out=None, batch=1, stream=None, is_async=False, coset_gen=None, ordering="NN",
+        columns_batch=False):
     """x: (batch*n, 4) uint64 numpy (host) or torch (device)."""
     total = x.shape[0]
     n = total // batch
     if out is None:
         out = np.zeros((total, 4), dtype=np.uint64) if isinstance(x, np.ndarray) else None
     kw = dict(batch_size=batch, are_inputs_on_device=_is_dev(x), are_outputs_on_device=_is_dev(out),
-              is_async=is_async, stream=stream)
+              is_async=is_async, stream=stream, ordering=ORDERINGS[ordering], columns_batch=columns_batch)
     if coset_gen is not None:
         kw["coset_gen"] = coset_gen
     cfg = ntt_config(**kw)

@@ -237,7 +237,14 @@ MBLS_DEV Fp<C> inv(const Fp<C>& a) {
     uint32_t e[C::N];
 #pragma unroll
     for (int i = 0; i < C::N; ++i) e[i] = C::MOD[i];
-    e[0] -= 2;  // both moduli are odd and > 2: no borrow
+    // m - 2 with borrow: r's low word is 0x00000001
+    uint32_t br = 2;
+#pragma unroll
+    for (int i = 0; i < C::N; ++i) {
+        const uint32_t d = e[i] - br;
+        br = e[i] < br ? 1u : 0u;
+        e[i] = d;
+    }
     return pow_words<C, C::N>(a, e);
 }
 

@@ -1,4 +1,4 @@
-// ntt.hip -- radix-2 Fr NTT for CDNA4, natural order in and out.
+// ntt.hip -- radix-2 Fr NTT for CDNA4 (natural-order core; orderings / columns_batch by permutation).
 //
 // Semantics = the CPU path the prover uses (core/ntt.rs:1488-1603, midnight_curves best_fft):
 //   forward  X_j = sum_i x_i w^(ij),  inverse  x_i = n^-1 sum_j X_j w^(-ij),
@@ -394,14 +394,48 @@ __global__ void k_coset_scale(uint8_t* data, Fr g, size_t n, size_t total) {
     store<FrCfg>(data + 32 * i, v * acc);
 }
 
-// Full ICICLE-semantics NTT call: staging, batch, coset; natural ordering only.
+// Layout permutation (gather): out position q of layout (out_cols, out_rev) takes the element
+// of layout (in_cols, in_rev) holding the same (member b, natural index e).  *_cols: column-
+// major batch (element e of member b at e*batch + b); *_rev: bit-reversed element order.
+__global__ void k_perm(uint8_t* __restrict__ out, const uint8_t* __restrict__ in, int log_n, uint32_t batch,
+                       int out_cols, int out_rev, int in_cols, int in_rev) {
+    const size_t n = (size_t)1 << log_n;
+    const size_t total = n * batch;
+    for (size_t q = blockIdx.x * (size_t)blockDim.x + threadIdx.x; q < total; q += (size_t)gridDim.x * blockDim.x) {
+        const size_t b = out_cols ? q % batch : q >> log_n;
+        const size_t i = out_cols ? q / batch : q & (n - 1);
+        const size_t e = out_rev ? bitrev((uint32_t)i, log_n) : i;
+        const size_t pi = in_rev ? bitrev((uint32_t)e, log_n) : e;
+        const size_t src = in_cols ? pi * batch + b : (b << log_n) + pi;
+        store<FrCfg>(out + 32 * q, load<FrCfg>(in + 32 * src));
+    }
+}
+
+static eIcicleError launch_perm(uint8_t* out, const uint8_t* in, int log_n, int batch, bool out_cols, bool out_rev,
+                                bool in_cols, bool in_rev, hipStream_t st) {
+    const size_t total = ((size_t)1 << log_n) * (size_t)batch;
+    size_t blocks = (total + 255) / 256;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    hipLaunchKernelGGL(k_perm, dim3((unsigned)blocks), dim3(256), 0, st, out, in, log_n, (uint32_t)batch,
+                       out_cols ? 1 : 0, out_rev ? 1 : 0, in_cols ? 1 : 0, in_rev ? 1 : 0);
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
+}
+
+// Full ICICLE-semantics NTT call: staging, batch (row or columns_batch layout), coset,
+// orderings.  R = bit-reversed order; M ("mixed", implementation-defined in ICICLE) is
+// bit-reversed here too, so kNM -> kMN round-trips.  Non-natural layouts are permuted to
+// natural row-major around the natural-order transform (one extra HBM pass each).
 eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTConfig* cfg, mbls_fr_t* output,
                       const mbls_fr_t* coset_gen) {
     if (!input || !output || !cfg) return MBLS_INVALID_POINTER;
     int log_n = log2_exact(size);
     if (log_n < 0) return MBLS_INVALID_ARGUMENT;
-    if (cfg->ordering != MBLS_ORDERING_NN) return MBLS_API_NOT_IMPLEMENTED;
-    if (cfg->columns_batch) return MBLS_API_NOT_IMPLEMENTED;
+    const int ord = (int)cfg->ordering;
+    if (ord < MBLS_ORDERING_NN || ord > MBLS_ORDERING_MN) return MBLS_INVALID_ARGUMENT;
+    const bool in_rev = ord == MBLS_ORDERING_RN || ord == MBLS_ORDERING_RR || ord == MBLS_ORDERING_MN;
+    const bool out_rev = ord == MBLS_ORDERING_NR || ord == MBLS_ORDERING_RR || ord == MBLS_ORDERING_NM;
+    const bool cols = cfg->columns_batch;
     int batch = cfg->batch_size > 0 ? cfg->batch_size : 1;
     hipStream_t st = static_cast<hipStream_t>(cfg->stream);
     {
@@ -413,23 +447,8 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
         }
     }
     const size_t bytes = (size_t)size * 32 * (size_t)batch;
-    StreamCtx& ctx = stream_ctx(st);
-    std::lock_guard<std::mutex> lk(ctx.mu);
-    size_t need = 0;
-    if (!cfg->are_inputs_on_device) need += align_up(bytes);
-    if (!cfg->are_outputs_on_device) need += align_up(bytes);
-    ctx.arena.reset();
-    eIcicleError er = ctx.arena.reserve(need);
-    if (er != MBLS_SUCCESS) return er;
-    const uint8_t* din = reinterpret_cast<const uint8_t*>(input);
-    uint8_t* dout = reinterpret_cast<uint8_t*>(output);
-    if (!cfg->are_inputs_on_device) {
-        void* t = ctx.arena.take(bytes);
-        MBLS_TRY(hipMemcpyAsync(t, input, bytes, hipMemcpyHostToDevice, st));
-        din = static_cast<const uint8_t*>(t);
-    }
-    if (!cfg->are_outputs_on_device) dout = static_cast<uint8_t*>(ctx.arena.take(bytes));
-
+    const size_t total = (size_t)size * batch;
+    const bool inverse = (dir == MBLS_NTT_INVERSE);
     // coset: forward evaluates on g*H (pre-scale by g^i); inverse post-scales by g^-i
     bool coset = false;
     uint64_t g[4];
@@ -437,42 +456,61 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
         memcpy(g, coset_gen->limbs, 32);
         coset = !hfr_eq(g, HFR_ONE);
     }
-    const size_t total = (size_t)size * batch;
-    const bool inverse = (dir == MBLS_NTT_INVERSE);
-    if (coset && !inverse) {
-        if (din != dout) MBLS_TRY(hipMemcpyAsync(dout, din, bytes, hipMemcpyDeviceToDevice, st));
-        hipLaunchKernelGGL(k_coset_scale, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dout, to_dev(g),
-                           (size_t)size, total);
-        MBLS_TRY(hipGetLastError());
-        din = dout;
+    const bool perm_in = (in_rev || cols) && log_n > 0;
+    const bool perm_out = (out_rev || cols) && log_n > 0;
+    const bool in_dev = cfg->are_inputs_on_device, out_dev = cfg->are_outputs_on_device;
+    // the transform's source must be natural row-major, writable when coset-scaled, and
+    // distinct from its destination (the first pass gathers bit-reversed)
+    const bool same = in_dev && out_dev && input == output;
+    const bool work_in_tmp = perm_in || (coset && !inverse) || (same && !perm_out);
+
+    StreamCtx& ctx = stream_ctx(st);
+    std::lock_guard<std::mutex> lk(ctx.mu);
+    size_t need = 0;
+    if (!in_dev) need += align_up(bytes);
+    if (!out_dev) need += align_up(bytes);
+    if (work_in_tmp) need += align_up(bytes);
+    if (perm_out) need += align_up(bytes);
+    ctx.arena.reset();
+    eIcicleError er = ctx.arena.reserve(need);
+    if (er != MBLS_SUCCESS) return er;
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(input);
+    uint8_t* dst = reinterpret_cast<uint8_t*>(output);
+    if (!in_dev) {
+        void* t = ctx.arena.take(bytes);
+        MBLS_TRY(hipMemcpyAsync(t, input, bytes, hipMemcpyHostToDevice, st));
+        src = static_cast<const uint8_t*>(t);
     }
-    if (din == dout && log_n > 0) {
-        // the first pass gathers bit-reversed: needs a distinct source
-        void* t = nullptr;
-        // in-place request: copy the input aside (arena grows once; keeps earlier pointers
-        // valid because growth only happens before any take in this call)
-        ctx.arena.reset();
-        size_t need2 = need + align_up(bytes);
-        er = ctx.arena.reserve(need2);
-        if (er != MBLS_SUCCESS) return er;
-        // re-take in the same order so previous pointers stay identical
-        if (!cfg->are_inputs_on_device) ctx.arena.take(bytes);
-        if (!cfg->are_outputs_on_device) ctx.arena.take(bytes);
-        t = ctx.arena.take(bytes);
-        MBLS_TRY(hipMemcpyAsync(t, din, bytes, hipMemcpyDeviceToDevice, st));
-        din = static_cast<const uint8_t*>(t);
+    if (!out_dev) dst = static_cast<uint8_t*>(ctx.arena.take(bytes));
+    uint8_t* wout = perm_out ? static_cast<uint8_t*>(ctx.arena.take(bytes)) : dst;
+    const uint8_t* win = src;
+    if (work_in_tmp) {
+        uint8_t* t = static_cast<uint8_t*>(ctx.arena.take(bytes));
+        if (perm_in) {
+            if ((er = launch_perm(t, src, log_n, batch, false, false, cols, in_rev, st)) != MBLS_SUCCESS) return er;
+        } else {
+            MBLS_TRY(hipMemcpyAsync(t, src, bytes, hipMemcpyDeviceToDevice, st));
+        }
+        if (coset && !inverse) {
+            hipLaunchKernelGGL(k_coset_scale, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, t, to_dev(g),
+                               (size_t)size, total);
+            MBLS_TRY(hipGetLastError());
+        }
+        win = t;
     }
-    er = ntt_device(dout, din, log_n, inverse, batch, st);
+    er = ntt_device(wout, win, log_n, inverse, batch, st);
     if (er != MBLS_SUCCESS) return er;
     if (coset && inverse) {
         uint64_t gi[4];
         hfr_inv(gi, g);
-        hipLaunchKernelGGL(k_coset_scale, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dout, to_dev(gi),
+        hipLaunchKernelGGL(k_coset_scale, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, wout, to_dev(gi),
                            (size_t)size, total);
         MBLS_TRY(hipGetLastError());
     }
-    if (!cfg->are_outputs_on_device) MBLS_TRY(hipMemcpyAsync(output, dout, bytes, hipMemcpyDeviceToHost, st));
-    if (!cfg->is_async || !cfg->are_outputs_on_device || !cfg->are_inputs_on_device) MBLS_TRY(hipStreamSynchronize(st));
+    if (perm_out && (er = launch_perm(dst, wout, log_n, batch, cols, out_rev, false, false, st)) != MBLS_SUCCESS)
+        return er;
+    if (!out_dev) MBLS_TRY(hipMemcpyAsync(output, dst, bytes, hipMemcpyDeviceToHost, st));
+    if (!cfg->is_async || !out_dev || !in_dev) MBLS_TRY(hipStreamSynchronize(st));
     return MBLS_SUCCESS;
 }
 

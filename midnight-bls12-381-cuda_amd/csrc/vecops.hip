@@ -11,6 +11,8 @@
 // DESIGN.md for the measured rates.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "mbls_common.hpp"
 #include "mbls_field.hpp"
 
@@ -32,6 +34,69 @@ __global__ __launch_bounds__(256) void k_vecop(uint8_t* __restrict__ out, const 
         if constexpr (OP == VecOp::ScalarMul) r = s * y;
         if constexpr (OP == VecOp::ScalarAdd) r = s + y;
         store<FrCfg>(out + 32 * i, r);
+    }
+}
+
+// batched scalar ops: scalar k of `sv` (device) applies to batch member k; member of element
+// i is i / size (row layout) or i % batch (columns_batch: element j of member k at j*batch+k)
+template <VecOp OP>
+__global__ __launch_bounds__(256) void k_scalar_batch(uint8_t* __restrict__ out, const uint8_t* __restrict__ sv,
+                                                      const uint8_t* __restrict__ b, size_t size, uint32_t batch,
+                                                      int cols, size_t n) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) {
+        const size_t k = cols ? i % batch : i / size;
+        const Fr s = load<FrCfg>(sv + 32 * k);
+        const Fr y = load<FrCfg>(b + 32 * i);
+        store<FrCfg>(out + 32 * i, OP == VecOp::ScalarMul ? s * y : s + y);
+    }
+}
+
+// ---- sum reduction (vec_ops.cu:350-382, 479-524): per-block LDS tree, then one block
+__global__ __launch_bounds__(256) void k_sum_partial(uint8_t* __restrict__ out, const uint8_t* __restrict__ in,
+                                                     size_t n) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[256 * 32];
+    Fr acc = Fr::zero();
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        acc = acc + load<FrCfg>(in + 32 * i);
+    store<FrCfg>(sh + 32 * threadIdx.x, acc);
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            acc = acc + load<FrCfg>(sh + 32 * (threadIdx.x + s));
+            store<FrCfg>(sh + 32 * threadIdx.x, acc);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) store<FrCfg>(out + 32 * blockIdx.x, acc);
+}
+
+// ---- batch inversion (vec_ops.cu:606-673 batch_inv_cuda): Montgomery's trick per thread
+// over a contiguous chunk, one Fermat inversion per chunk; zero inputs map to zero (field_inv
+// semantics, field.cuh:750-900).  `out` holds the prefix products between the two sweeps.
+static constexpr int INV_CHUNK = 64;
+__global__ __launch_bounds__(256) void k_batch_inv(uint8_t* __restrict__ out, const uint8_t* __restrict__ in,
+                                                   size_t n) {
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t s = t * INV_CHUNK;
+    if (s >= n) return;
+    const size_t e = s + INV_CHUNK < n ? s + INV_CHUNK : n;
+    Fr acc = Fr::one();
+    for (size_t i = s; i < e; ++i) {
+        const Fr x = load<FrCfg>(in + 32 * i);
+        store<FrCfg>(out + 32 * i, acc);
+        if (!x.is_zero()) acc = acc * x;
+    }
+    Fr inv_acc = inv(acc);
+    for (size_t i = e; i-- > s;) {
+        const Fr x = load<FrCfg>(in + 32 * i);
+        if (x.is_zero()) {
+            store<FrCfg>(out + 32 * i, Fr::zero());
+        } else {
+            store<FrCfg>(out + 32 * i, inv_acc * load<FrCfg>(out + 32 * i));
+            inv_acc = inv_acc * x;
+        }
     }
 }
 
@@ -80,7 +145,7 @@ static eIcicleError run_vec_op(const mbls_fr_t* a, const mbls_fr_t* b, size_t si
     if (!scalar_op && !cfg->is_a_on_device) need += align_up(bytes);
     if (!cfg->is_b_on_device) need += align_up(bytes);
     if (!cfg->is_result_on_device) need += align_up(bytes);
-    if (scalar_op && cfg->is_a_on_device) need += align_up(32 * (size_t)batch);
+    if (scalar_op && !cfg->is_a_on_device) need += align_up(32 * (size_t)batch);
     ctx.arena.reset();
     eIcicleError er = ctx.arena.reserve(need);
     if (er != MBLS_SUCCESS) return er;
@@ -101,19 +166,16 @@ static eIcicleError run_vec_op(const mbls_fr_t* a, const mbls_fr_t* b, size_t si
     if (!cfg->is_result_on_device) dout = static_cast<uint8_t*>(ctx.arena.take(bytes));
 
     if (scalar_op) {
-        // one scalar per batch entry (ICICLE v4 batched scalar ops)
-        std::vector<mbls_fr_t> hs(batch);
-        if (cfg->is_a_on_device) {
-            MBLS_TRY(hipMemcpyAsync(hs.data(), a, 32 * (size_t)batch, hipMemcpyDeviceToHost, st));
-            MBLS_TRY(hipStreamSynchronize(st));
-        } else {
-            for (int k = 0; k < batch; ++k) hs[k] = a[k];
+        // one scalar per batch entry (ICICLE v4 batched scalar ops), read on device
+        const uint8_t* sv = reinterpret_cast<const uint8_t*>(a);
+        if (!cfg->is_a_on_device) {
+            void* t = ctx.arena.take(32 * (size_t)batch);
+            MBLS_TRY(hipMemcpyAsync(t, a, 32 * (size_t)batch, hipMemcpyHostToDevice, st));
+            sv = static_cast<const uint8_t*>(t);
         }
-        for (int k = 0; k < batch; ++k) {
-            er = launch<OP>(dout + (size_t)k * size * 32, nullptr, db + (size_t)k * size * 32, fr_from_host(&hs[k]),
-                            size, st);
-            if (er != MBLS_SUCCESS) return er;
-        }
+        hipLaunchKernelGGL(k_scalar_batch<OP>, dim3(vec_grid(total)), dim3(256), 0, st, dout, sv, db, size,
+                           (uint32_t)batch, cfg->columns_batch ? 1 : 0, total);
+        MBLS_TRY(hipGetLastError());
     } else {
         er = launch<OP>(dout, da, db, Fr{}, total, st);
         if (er != MBLS_SUCCESS) return er;
@@ -121,6 +183,55 @@ static eIcicleError run_vec_op(const mbls_fr_t* a, const mbls_fr_t* b, size_t si
     if (!cfg->is_result_on_device) MBLS_TRY(hipMemcpyAsync(output, dout, bytes, hipMemcpyDeviceToHost, st));
     if (!cfg->is_async || !cfg->is_result_on_device || !cfg->is_a_on_device || !cfg->is_b_on_device)
         MBLS_TRY(hipStreamSynchronize(st));
+    return MBLS_SUCCESS;
+}
+
+// sum of `size` device elements -> output (device or host per is_result_on_device)
+static eIcicleError vec_sum(mbls_fr_t* output, const mbls_fr_t* input, int size, const VecOpsConfig* cfg) {
+    if (!output || !input || !cfg) return MBLS_INVALID_POINTER;
+    if (size < 0) return MBLS_INVALID_ARGUMENT;
+    hipStream_t st = static_cast<hipStream_t>(cfg->stream);
+    StreamCtx& ctx = stream_ctx(st);
+    std::lock_guard<std::mutex> lk(ctx.mu);
+    const int blocks = size > 0 ? std::min(vec_grid((size_t)size), 1024) : 1;
+    ctx.arena.reset();
+    eIcicleError er = ctx.arena.reserve(align_up(32 * (size_t)blocks) + align_up(32));
+    if (er != MBLS_SUCCESS) return er;
+    uint8_t* part = static_cast<uint8_t*>(ctx.arena.take(32 * (size_t)blocks));
+    uint8_t* res = static_cast<uint8_t*>(ctx.arena.take(32));
+    hipLaunchKernelGGL(k_sum_partial, dim3(blocks), dim3(256), 0, st, part, reinterpret_cast<const uint8_t*>(input),
+                       (size_t)size);
+    hipLaunchKernelGGL(k_sum_partial, dim3(1), dim3(256), 0, st, res, part, (size_t)blocks);
+    MBLS_TRY(hipGetLastError());
+    MBLS_TRY(hipMemcpyAsync(output, res, 32, cfg->is_result_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                            st));
+    if (!cfg->is_async || !cfg->is_result_on_device) MBLS_TRY(hipStreamSynchronize(st));
+    return MBLS_SUCCESS;
+}
+
+// element-wise inverses of `size` device elements into device `output` (in place allowed:
+// the inputs are then copied aside, since `output` holds the prefix products)
+static eIcicleError batch_inv(mbls_fr_t* output, const mbls_fr_t* input, int size, const VecOpsConfig* cfg) {
+    if (!output || !input) return MBLS_INVALID_POINTER;
+    if (size < 0) return MBLS_INVALID_ARGUMENT;
+    if (size == 0) return MBLS_SUCCESS;
+    hipStream_t st = cfg ? static_cast<hipStream_t>(cfg->stream) : nullptr;
+    const uint8_t* in = reinterpret_cast<const uint8_t*>(input);
+    uint8_t* out = reinterpret_cast<uint8_t*>(output);
+    StreamCtx& ctx = stream_ctx(st);
+    std::lock_guard<std::mutex> lk(ctx.mu);
+    if (in == out) {  // in place: keep a copy of the inputs for the backward sweep
+        ctx.arena.reset();
+        eIcicleError er = ctx.arena.reserve(align_up(32 * (size_t)size));
+        if (er != MBLS_SUCCESS) return er;
+        uint8_t* t = static_cast<uint8_t*>(ctx.arena.take(32 * (size_t)size));
+        MBLS_TRY(hipMemcpyAsync(t, in, 32 * (size_t)size, hipMemcpyDeviceToDevice, st));
+        in = t;
+    }
+    const size_t threads = ((size_t)size + INV_CHUNK - 1) / INV_CHUNK;
+    hipLaunchKernelGGL(k_batch_inv, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, out, in, (size_t)size);
+    MBLS_TRY(hipGetLastError());
+    if (!cfg || !cfg->is_async) MBLS_TRY(hipStreamSynchronize(st));
     return MBLS_SUCCESS;
 }
 
@@ -184,6 +295,12 @@ eIcicleError scalar_mul_vec_cuda(mbls_fr_t* output, const mbls_fr_t* scalar, con
 eIcicleError scalar_add_vec_cuda(mbls_fr_t* output, const mbls_fr_t* scalar, const mbls_fr_t* vec, int size,
                                  const VecOpsConfig* config) {
     return raw_vec_op<VecOp::ScalarAdd>(output, scalar, vec, size, config);
+}
+eIcicleError vec_sum_cuda(mbls_fr_t* output, const mbls_fr_t* input, int size, const VecOpsConfig* config) {
+    return vec_sum(output, input, size, config);
+}
+eIcicleError bls12_381_batch_inv_cuda(mbls_fr_t* output, const mbls_fr_t* input, int size, const VecOpsConfig* config) {
+    return batch_inv(output, input, size, config);
 }
 
 }  // extern "C"

@@ -81,7 +81,104 @@ def test_vecops_empty_and_errors(amd):
     assert e.value.code == amd.INVALID_POINTER
 
 
+def _bitrev_perm(log_n):
+    n = 1 << log_n
+    return np.array([int(format(i, f"0{log_n}b")[::-1], 2) if log_n else 0 for i in range(n)], dtype=np.int64)
+
+
+@pytest.mark.parametrize("columns", [False, True])
+def test_vecops_batched_scalar_ops(amd, columns):
+    """ICICLE v4 batch: one scalar per member, row or columns_batch layout; host and device scalars"""
+    import torch
+    n, batch = 1000, 3
+    g = pr.rng(17)
+    vals = [g.randrange(pr.R) for _ in range(n * batch)]
+    sc = [g.randrange(pr.R) for _ in range(batch)]
+    b = H.ints_to_limbs(vals, 4)
+    s = H.ints_to_limbs(sc, 4)
+    member = [(i % batch) if columns else (i // n) for i in range(n * batch)]
+    for op, fn in (("scalar_mul", lambda x, y: pr.fr_mont_mul(x, y)), ("scalar_add", lambda x, y: (x + y) % pr.R)):
+        expect = [fn(sc[member[i]], v) for i, v in enumerate(vals)]
+        out = amd.vec_op(op, s, b, batch=batch, columns_batch=columns)
+        assert H.limbs_to_ints(out) == expect, op
+        out_d = torch.zeros((n * batch, 4), dtype=torch.int64, device="cuda")
+        amd.vec_op(op, amd.torch_u64(s), amd.torch_u64(b), out=out_d, batch=batch, columns_batch=columns)
+        torch.cuda.synchronize()
+        assert H.limbs_to_ints(amd.to_numpy_u64(out_d)) == expect, op
+
+
+@pytest.mark.parametrize("n", [1, 5, 256, 1000, 1 << 16])
+def test_vec_sum(amd, n):
+    g = pr.rng(n)
+    vals = [g.randrange(pr.R) for _ in range(n)]
+    out = amd.vec_sum(amd.torch_u64(H.ints_to_limbs(vals, 4)))
+    assert H.limbs_to_ints(out)[0] == sum(vals) % pr.R
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4097])
+def test_batch_inv(amd, n):
+    """Montgomery-form inverses (x R -> x^-1 R), zeros map to zero; out of place and in place"""
+    import torch
+    g = pr.rng(100 + n)
+    xs = [g.randrange(pr.R) for _ in range(n)]
+    for k in range(0, n, 7):
+        xs[k] = 0
+    mont = [pr.fr_to_mont(v) for v in xs]
+    expect = [pr.fr_to_mont(pow(v, -1, pr.R)) if v else 0 for v in xs]
+    x = amd.torch_u64(H.ints_to_limbs(mont, 4))
+    out = torch.zeros_like(x)
+    amd.batch_inv(x, out)
+    torch.cuda.synchronize()
+    assert H.limbs_to_ints(amd.to_numpy_u64(out)) == expect
+    amd.batch_inv(x, x)
+    torch.cuda.synchronize()
+    assert H.limbs_to_ints(amd.to_numpy_u64(x)) == expect
+
+
 # ----------------------------------------------------------------------------- NTT
+@pytest.mark.parametrize("ordering", ["NN", "NR", "RN", "RR", "NM", "MN"])
+def test_ntt_orderings(amd, ordering):
+    """R (and M, defined as bit-reversed) on the input and/or output side, both directions"""
+    amd.ntt_init_domain()
+    log_n = 9
+    n = 1 << log_n
+    g = pr.rng(31)
+    x = H.ints_to_limbs([pr.fr_to_mont(g.randrange(pr.R)) for _ in range(n)], 4)
+    rev = _bitrev_perm(log_n)
+    in_rev = ordering[0] in "RM"
+    out_rev = ordering[1] in "RM"
+    for inverse in (False, True):
+        got = amd.ntt(x[rev] if in_rev else x, inverse=inverse, ordering=ordering)
+        ref = H.oracle_ntt(x, log_n, inverse)
+        assert np.array_equal(got, ref[rev] if out_rev else ref), (ordering, inverse)
+    # NR forward then RN inverse round-trips without any explicit permutation
+    y = amd.ntt(x, ordering="NR")
+    assert np.array_equal(amd.ntt(y, inverse=True, ordering="RN"), x)
+
+
+@pytest.mark.parametrize("ordering", ["NN", "RR"])
+def test_ntt_columns_batch(amd, ordering):
+    """columns_batch: element i of polynomial b at i*batch + b (host and device buffers)"""
+    import torch
+    amd.ntt_init_domain()
+    log_n, batch = 8, 3
+    n = 1 << log_n
+    g = pr.rng(41)
+    polys = [H.ints_to_limbs([pr.fr_to_mont(g.randrange(pr.R)) for _ in range(n)], 4) for _ in range(batch)]
+    rev = _bitrev_perm(log_n)
+    r = ordering == "RR"
+    inter = np.stack([p[rev] if r else p for p in polys], axis=1).reshape(n * batch, 4)
+    for inverse in (False, True):
+        expect = np.stack([(lambda o: o[rev] if r else o)(H.oracle_ntt(p, log_n, inverse)) for p in polys],
+                          axis=1).reshape(n * batch, 4)
+        got = amd.ntt(np.ascontiguousarray(inter), inverse=inverse, batch=batch, ordering=ordering, columns_batch=True)
+        assert np.array_equal(got, expect), inverse
+        d = amd.torch_u64(np.ascontiguousarray(inter))
+        amd.ntt(d, inverse=inverse, out=d, batch=batch, ordering=ordering, columns_batch=True)  # in place
+        torch.cuda.synchronize()
+        assert np.array_equal(amd.to_numpy_u64(d), expect), inverse
+
+
 def test_ntt_golden(amd):
     amd.ntt_init_domain()
     g = H.load_golden("ntt.json")
@@ -329,3 +426,24 @@ def test_msm_glv_split_boundaries(amd, gh):
     ref = H.g1_from_affine_mont(H.oracle_msm("g1", small, bn))
     r = amd.msm("g1", small, bn, bitsize=128, n=n)
     assert gh.decode_icicle("g1", r[0]) == ref
+
+
+@pytest.mark.slow
+def test_msm_g1_2_24_bit_exact(amd, gh):
+    """north-star size: G1 MSM of 2^24 points (BASELINE config #4 total size, single GPU) equals
+    the oracle's multithreaded Pippenger bit-exactly (canonical affine)"""
+    import torch
+    n = 1 << 24
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0004, montgomery=True)
+    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 0x5EED0013)
+    out = torch.zeros((1, 18), dtype=torch.int64, device="cuda")
+    amd.msm("g1", s, b, scalars_mont=True, out=out)
+    torch.cuda.synchronize()
+    got = gh.decode_icicle("g1", amd.to_numpy_u64(out)[0])
+    del s
+    s_std = np.zeros((n, 4), dtype=np.uint64)
+    H.oracle().orc_gen_scalars(H.ptr(s_std), 0x5EED0004, n)
+    ref = H.oracle_msm("g1", s_std, amd.to_numpy_u64(b), threads=16)
+    assert got == H.g1_from_affine_mont(ref)
