@@ -26,6 +26,18 @@ sys.path.insert(0, PKG)
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 MSM_BYTES_PER_POINT = 128  # 32 B scalar + 96 B affine base
 NTT_BYTES_PER_ELEM = 64    # one read + one write of 32 B per transform
+# HBM bytes per launch from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+# (tools/gpu_pmc.sh on tools/pmc_probe.py's fixed workload; gfx950 FETCH_SIZE x2 correction)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+
+
+def pmc_traffic(kernel, n_launches_per_unit=1):
+    try:
+        with open(PMC_SUMMARY) as f:
+            k = json.load(f)["kernels"].get(kernel)
+        return None if not k or k.get("hbm_bytes_per_launch") is None else k["hbm_bytes_per_launch"] * n_launches_per_unit
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def parse():
@@ -37,6 +49,8 @@ def parse():
     ap.add_argument("--ntt-log", type=int, default=22)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-mix", action="store_true", help="skip the G2 MSM + batched NTT overlap leg (config #5)")
+    ap.add_argument("--mix-batch", type=int, default=4, help="NTT polynomials in the config #5 batch")
     return ap.parse_args()
 
 
@@ -130,6 +144,29 @@ def main():
     ntt_prof = amd.profile_read()
     amd.profile(False)
 
+    # NTT 2^20 forward + inverse round trip (BASELINE config #2), device-resident
+    x20 = x[: 1 << 20]
+    y20 = torch.zeros_like(x20)
+    z20 = torch.zeros_like(x20)
+    reps = max(3, args.steps)
+    for _ in range(2):
+        amd.ntt(x20, out=y20, stream=stream, is_async=True)
+        amd.ntt(y20, inverse=True, out=z20, stream=stream, is_async=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        amd.ntt(x20, out=y20, stream=stream, is_async=True)
+        amd.ntt(y20, inverse=True, out=z20, stream=stream, is_async=True)
+    torch.cuda.synchronize(dev)
+    ntt20_rt_ms = (time.perf_counter() - t0) / reps * 1e3
+    ntt20_exact = bool(torch.equal(z20, x20))
+    del y20, z20
+
+    # ------------------------------------------------------------------ config #5 mix (replicas)
+    mix = None
+    if not args.no_mix:
+        mix = mix_leg(args, amd, torch, dev, rank)
+
     # ------------------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -170,17 +207,74 @@ def main():
                          "bound": "hbm", "achieved": round(msm_ach, 2) if msm_ach else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(msm_ach / HBM_PEAK_GBS, 5) if msm_ach else None,
-                         "traffic": None,
+                         "traffic": pmc_traffic("k_accumulate"),
+                         "traffic_source": "profiles/r01/pmc_summary.json (bytes per launch)",
                          "note": "VALU-bound (v_mad_u64_u32); HBM fraction reported as the contract asks"},
+            "ntt20_roundtrip_ms": round(ntt20_rt_ms, 4),
+            "ntt20_roundtrip_exact": ntt20_exact,
+            "mix_g2msm_batched_ntt": mix,
             "roofline_ntt": {"kernel": "k_ntt_pass x passes (one transform)", "bound": "hbm",
                              "achieved": round(ntt_ach, 2) if ntt_ach else None, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(ntt_ach / HBM_PEAK_GBS, 5) if ntt_ach else None,
-                             "traffic": None, "pass_ms": round(ntt_pass_ms, 4) if ntt_pass_ms else None},
+                             "traffic": ntt_traffic(args.ntt_log),
+                             "traffic_source": "profiles/r01/pmc_summary.json (first + later passes)",
+                             "pass_ms": round(ntt_pass_ms, 4) if ntt_pass_ms else None},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def ntt_traffic(log_n):
+    """HBM bytes of one 2^22 transform: first pass + (passes - 1) later passes (pmc_probe sizes)"""
+    if log_n != 22:
+        return None
+    first, later = pmc_traffic("k_ntt_pass<true, false>"), pmc_traffic("k_ntt_pass<false, false>")
+    return None if first is None or later is None else first + 2 * later
+
+
+def mix_leg(args, amd, torch, dev, rank):
+    """BASELINE config #5: G2 MSM 2^msm_log and a batch of Fr NTTs 2^ntt_log enqueued on two
+    HIP streams at once (PLONK-prover-shaped mix); reports each alone and the overlapped wall."""
+    n = 1 << args.msm_log
+    nn = 1 << args.ntt_log
+    B = args.mix_batch
+    s_a = torch.cuda.Stream(dev)
+    s_b = torch.cuda.Stream(dev)
+    sc = torch.zeros((n, 4), dtype=torch.int64, device=dev)
+    bs = torch.zeros((n, 24), dtype=torch.int64, device=dev)
+    amd.gen_scalars(sc, 0x5EED0005 + rank, montgomery=True, stream=s_a)
+    amd.gen_bases("g2", bs, 0x5EED0015 + rank, stream=s_a)
+    res = torch.zeros((1, 36), dtype=torch.int64, device=dev)
+    xb = torch.zeros((B * nn, 4), dtype=torch.int64, device=dev)
+    yb = torch.zeros_like(xb)
+    amd.gen_scalars(xb, 0x5EED0025 + rank, montgomery=True, stream=s_b)
+    torch.cuda.synchronize(dev)
+
+    def g2():
+        amd.msm("g2", sc, bs, icicle=False, scalars_mont=True, out=res, stream=s_a, is_async=True, n=n)
+
+    def ntts():
+        amd.ntt(xb, out=yb, batch=B, stream=s_b, is_async=True)
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    reps = max(2, min(args.steps, 5))
+    g2_ms = timed(g2, reps)
+    ntt_ms = timed(ntts, reps)
+    both_ms = timed(lambda: (g2(), ntts()), reps)
+    return {"g2_msm_points": n, "ntt_batch": B, "ntt_size": nn, "g2_msm_ms": round(g2_ms, 3),
+            "g2_msm_per_sec": round(1e3 / g2_ms, 3), "batched_ntt_ms": round(ntt_ms, 3),
+            "overlapped_ms": round(both_ms, 3), "sum_isolated_ms": round(g2_ms + ntt_ms, 3),
+            "streams": 2}
 
 
 def cpu_baseline(args, amd, scalars, bases, n):

@@ -8,9 +8,11 @@
 // (SURVEY.md finding 2); we do not reproduce that.
 //
 // Data layout in HBM: n contiguous 32-byte Fr values per polynomial, batch polynomials
-// back to back (columns_batch = false).  Twiddle table: w_K^i, i < 2^(K-1), Montgomery, plus
-// the inverse table, K = the domain's max log size (twiddle of stage m = 2^s, index j is
-// table[j * 2^(K-s)]).
+// back to back (other layouts are permuted in and out).  Twiddles: per-stage tables
+// concatenated, stage s (m = 2^s) holding w_(2^s)^i, i < 2^(s-1), at offset 2^(s-1) - 1
+// (2^L - 1 entries for stages 1..L), so adjacent columns of a tile read adjacent twiddles.
+// (A single w_(2^K)^i table read at stride 2^(K-s) put every lane on its own cache line:
+// measured 3.5x the data bytes fetched by the later passes, profiles/r01.)
 //
 // Kernel structure: ceil(k / 10) passes, each a LDS-resident tile of T = 1024 elements
 // (32 KiB) doing up to 10 radix-2 DIT stages between __syncthreads.  Pass 1 fuses the
@@ -41,9 +43,10 @@ static const uint64_t ROOT_2_32_MONT[4] = {0xb9b58d8c5f0e466aULL, 0x5b1b4c801819
                                            0x5bf3adda19e9b27bULL};
 
 struct Domain {
-    int max_log = 0;
-    uint8_t* tw = nullptr;      // w^i, i < 2^(max_log-1)
-    uint8_t* tw_inv = nullptr;  // w^-i
+    int order_log = 32;         // 2^order_log: order of the initialised root (size bound)
+    int max_log = 0;            // stage tables built for stages 1..max_log
+    uint8_t* tw = nullptr;      // per-stage w_(2^s)^i tables (see header)
+    uint8_t* tw_inv = nullptr;  // per-stage w_(2^s)^-i
 };
 
 static std::mutex g_domain_mu;
@@ -53,19 +56,22 @@ __device__ __forceinline__ uint32_t bitrev(uint32_t x, int bits) {
     return bits == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - bits));
 }
 
-// table[i] = w^i for i < count (one exponentiation per entry: init only)
-__global__ void k_twiddles(uint8_t* table, Fr w, uint32_t count) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
+// per-stage tables: entry g (stage s = floor(log2(g+1)) + 1, i = g + 1 - 2^(s-1)) holds
+// w_(2^L)^(i * 2^(L-s)) = w_(2^s)^i; one exponentiation per entry (init only)
+__global__ void k_twiddles(uint8_t* table, Fr w, int L, uint32_t count) {
+    uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= count) return;
+    const int s = 32 - __builtin_clz(g + 1);  // floor(log2(g+1)) + 1
+    const uint32_t i = g + 1 - (1u << (s - 1));
     Fr acc = Fr::one();
     Fr b = w;
-    uint32_t e = i;
+    uint64_t e = (uint64_t)i << (L - s);
     while (e) {
         if (e & 1) acc = acc * b;
         b = sqr(b);
         e >>= 1;
     }
-    store<FrCfg>(table + 32 * (size_t)i, acc);
+    store<FrCfg>(table + 32 * (size_t)g, acc);
 }
 
 // One pass of up to NTT_TILE_LOG DIT stages.
@@ -74,7 +80,7 @@ __global__ void k_twiddles(uint8_t* table, Fr w, uint32_t count) {
 template <bool FIRST, bool SCALE>
 __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ out, const uint8_t* __restrict__ in,
                                                           const uint8_t* __restrict__ tw, int log_n, int s0, int L,
-                                                          int logC, int tw_log, Fr scale) {
+                                                          int logC, Fr scale) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[NTT_TILE * 32];
     const int C = 1 << logC;
     const int rows = 1 << L;
@@ -127,7 +133,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ 
             Fr b = load<FrCfg>(lds + 32 * (t1 * C + c));
             if (l > 1 || !FIRST) {
                 size_t jj = ((size_t)j << s0) + (FIRST ? 0 : lo_base + c);
-                Fr w = load<FrCfg>(tw + 32 * (jj << (tw_log - s)));
+                Fr w = load<FrCfg>(tw + 32 * ((((size_t)1 << (s - 1)) - 1) + jj));
                 b = b * w;
             }
             store<FrCfg>(lds + 32 * (t0 * C + c), a + b);
@@ -269,9 +275,13 @@ static eIcicleError build_domain(int max_log, hipStream_t st) {
         MBLS_TRY(hipDeviceSynchronize());
         (void)hipFree(g_domain.tw);
         (void)hipFree(g_domain.tw_inv);
-        g_domain = Domain{};
+        g_domain.tw = g_domain.tw_inv = nullptr;
+        g_domain.max_log = 0;
     }
-    size_t count = max_log > 0 ? ((size_t)1 << (max_log - 1)) : 1;
+    const int order = g_domain.order_log;
+    if (max_log > order) return MBLS_INVALID_ARGUMENT;
+    size_t count = ((size_t)1 << max_log) - 1;
+    if (count == 0) count = 1;
     uint8_t *tw = nullptr, *twi = nullptr;
     MBLS_TRY(hipMalloc(&tw, 32 * count));
     hipError_t e2 = hipMalloc(&twi, 32 * count);
@@ -283,8 +293,8 @@ static eIcicleError build_domain(int max_log, hipStream_t st) {
     canonical_omega(w, max_log);
     hfr_inv(wi, w);
     int blocks = (int)((count + 255) / 256);
-    hipLaunchKernelGGL(k_twiddles, dim3(blocks), dim3(256), 0, st, tw, to_dev(w), (uint32_t)count);
-    hipLaunchKernelGGL(k_twiddles, dim3(blocks), dim3(256), 0, st, twi, to_dev(wi), (uint32_t)count);
+    hipLaunchKernelGGL(k_twiddles, dim3(blocks), dim3(256), 0, st, tw, to_dev(w), max_log, (uint32_t)count);
+    hipLaunchKernelGGL(k_twiddles, dim3(blocks), dim3(256), 0, st, twi, to_dev(wi), max_log, (uint32_t)count);
     MBLS_TRY(hipGetLastError());
     MBLS_TRY(hipStreamSynchronize(st));
     g_domain.max_log = max_log;
@@ -331,13 +341,13 @@ eIcicleError ntt_device(uint8_t* out, const uint8_t* in, int log_n, bool inverse
         if (tiles > 0x7fffffff) return MBLS_INVALID_ARGUMENT;
         dim3 grid((unsigned)tiles), blk(NTT_THREADS);
         if (first && last && inverse)
-            hipLaunchKernelGGL((k_ntt_pass<true, true>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, D.max_log, scale);
+            hipLaunchKernelGGL((k_ntt_pass<true, true>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
         else if (first)
-            hipLaunchKernelGGL((k_ntt_pass<true, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, D.max_log, scale);
+            hipLaunchKernelGGL((k_ntt_pass<true, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
         else if (last && inverse)
-            hipLaunchKernelGGL((k_ntt_pass<false, true>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, D.max_log, scale);
+            hipLaunchKernelGGL((k_ntt_pass<false, true>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
         else
-            hipLaunchKernelGGL((k_ntt_pass<false, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, D.max_log, scale);
+            hipLaunchKernelGGL((k_ntt_pass<false, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
         MBLS_TRY(hipGetLastError());
         s0 += L;
     }
@@ -363,9 +373,10 @@ eIcicleError ntt_init_domain(const mbls_fr_t* root, const NTTInitDomainConfig* c
         K = hfr_log_order(m);
     }
     if (K < 0) return MBLS_INVALID_ARGUMENT;
-    if (K > 27) K = 27;  // 2^27 Fr twiddles = 4 GiB per table: cap the eager tables
     std::lock_guard<std::mutex> lk(g_domain_mu);
-    return build_domain(K, st);
+    g_domain.order_log = K;
+    // stage tables up to 2^22 now (2 x 128 MiB); larger sizes extend them on first use
+    return build_domain(K < 22 ? K : 22, st);
 }
 
 eIcicleError ntt_release_domain() {
@@ -440,9 +451,12 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
     hipStream_t st = static_cast<hipStream_t>(cfg->stream);
     {
         std::lock_guard<std::mutex> lk(g_domain_mu);
+        if (log_n > g_domain.order_log) return MBLS_INVALID_ARGUMENT;  // beyond the initialised root
         if (!g_domain.tw || g_domain.max_log < log_n) {
-            // lazily size the domain (the Rust side initialises once with its max size)
-            eIcicleError er = build_domain(log_n < 20 ? 20 : log_n, st);
+            // lazily extend the stage tables (init_domain builds up to 2^22)
+            int want = log_n < 20 ? 20 : log_n;
+            if (want > g_domain.order_log) want = g_domain.order_log;
+            eIcicleError er = build_domain(want, st);
             if (er != MBLS_SUCCESS) return er;
         }
     }
