@@ -568,12 +568,17 @@ eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint3
     return MBLS_SUCCESS;
 }
 
-// chunks per bucket; nchunks[m] receives the maximum (drives the heavy-bucket tree passes)
-__global__ void k_chunk_counts(const uint32_t* __restrict__ counts, uint32_t* __restrict__ nchunks, uint32_t m) {
+// Chunks are 16-ALIGNED in the sorted array (chunk t = positions [16t, 16t + 16)), so every
+// accumulation thread does exactly 16 additions; a chunk crossing bucket boundaries yields one
+// partial ("segment") per bucket it touches.  Segments of bucket b: the aligned chunks that
+// overlap [off_b, off_b + cnt_b).  nchunks[m] receives the maximum (heavy-bucket passes).
+__global__ void k_chunk_counts(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offsets,
+                               uint32_t* __restrict__ nchunks, uint32_t m) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t c = 0;
     if (b < m) {
-        c = (counts[b] + CHUNK - 1) / CHUNK;
+        const uint32_t cnt = counts[b], o = offsets[b];
+        c = cnt ? (o + cnt - 1) / CHUNK - o / CHUNK + 1 : 0u;
         nchunks[b] = c;
     }
     // wave max, one atomic per wave
@@ -581,9 +586,10 @@ __global__ void k_chunk_counts(const uint32_t* __restrict__ counts, uint32_t* __
     if ((threadIdx.x & 63) == 0 && c > 1) atomicMax(&nchunks[m], c);
 }
 
-eIcicleError launch_chunk_counts(const uint32_t* counts, uint32_t* nchunks, uint32_t m, hipStream_t st) {
+eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
+                                 hipStream_t st) {
     MBLS_TRY(hipMemsetAsync(nchunks + m, 0, 4, st));
-    hipLaunchKernelGGL(k_chunk_counts, dim3((m + 255) / 256), dim3(256), 0, st, counts, nchunks, m);
+    hipLaunchKernelGGL(k_chunk_counts, dim3((m + 255) / 256), dim3(256), 0, st, counts, offsets, nchunks, m);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }
@@ -609,14 +615,19 @@ eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const ui
     return MBLS_SUCCESS;
 }
 
-__global__ void k_chunk_owner(const uint32_t* __restrict__ chunk_off, uint32_t m, uint32_t* __restrict__ owner) {
+// owner[segment] = bucket; first[t] = the bucket holding position 16t (the start of chunk t)
+__global__ void k_chunk_owner(const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ offsets, uint32_t m,
+                              uint32_t* __restrict__ owner, uint32_t* __restrict__ first) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
     for (uint32_t k = chunk_off[b]; k < chunk_off[b + 1]; ++k) owner[k] = b;
+    const uint32_t o = offsets[b], e = offsets[b + 1];
+    for (uint32_t t = (o + CHUNK - 1) / CHUNK; t * CHUNK < e; ++t) first[t] = b;
 }
 
-eIcicleError launch_chunk_owner(const uint32_t* chunk_off, uint32_t m, uint32_t* owner, hipStream_t st) {
-    hipLaunchKernelGGL(k_chunk_owner, dim3((m + 255) / 256), dim3(256), 0, st, chunk_off, m, owner);
+eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offsets, uint32_t m, uint32_t* owner,
+                                uint32_t* first, hipStream_t st) {
+    hipLaunchKernelGGL(k_chunk_owner, dim3((m + 255) / 256), dim3(256), 0, st, chunk_off, offsets, m, owner, first);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }

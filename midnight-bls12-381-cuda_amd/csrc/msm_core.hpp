@@ -69,29 +69,35 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
                            uint32_t* vals, uint32_t* ranks, uint32_t* counts, uint8_t* dsrc, hipStream_t st);
 size_t digits_src_bytes(uint32_t n);
 eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint32_t* tmp, hipStream_t st);
-eIcicleError launch_chunk_counts(const uint32_t* counts, uint32_t* nchunks, uint32_t m, hipStream_t st);
+eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
+                                 hipStream_t st);
 eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const uint32_t* ranks, size_t total,
                             const uint32_t* offsets, uint32_t* sorted, hipStream_t st);
-eIcicleError launch_chunk_owner(const uint32_t* chunk_off, uint32_t m, uint32_t* owner, hipStream_t st);
+eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offsets, uint32_t m, uint32_t* owner,
+                                uint32_t* first, hipStream_t st);
 eIcicleError launch_scalars_from_mont(uint8_t* s, size_t n, hipStream_t st);
 eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
 size_t scan_tmp_words(uint32_t m);
 
 // ------------------------------------------------------------------------------------
-// 4. accumulation: one thread per chunk of one bucket
+// 4. accumulation: thread t sums the 16 contributions at sorted positions [16t, 16t + 16),
+//    one partial per bucket segment it touches (see k_chunk_counts): no idle lanes on the
+//    short last chunk of each bucket.
 // ------------------------------------------------------------------------------------
 template <class F>
 __global__ __launch_bounds__(256) void k_accumulate(const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ chunk_off,
-                                                    const uint32_t* __restrict__ owner, uint32_t TB, uint32_t max_chunks,
+                                                    const uint32_t* __restrict__ first, uint32_t TB,
                                                     const uint8_t* __restrict__ bases, const uint8_t* __restrict__ phi,
                                                     uint32_t nsplit, uint8_t* __restrict__ partials) {
-    uint32_t ch = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ch >= max_chunks || ch >= chunk_off[TB]) return;
-    uint32_t b = owner[ch];
-    uint32_t k = ch - chunk_off[b];
-    uint32_t beg = offsets[b] + k * CHUNK;
-    uint32_t end = min(beg + CHUNK, offsets[b + 1]);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t total = offsets[TB];
+    const uint32_t beg = t * CHUNK;
+    if (beg >= total) return;
+    const uint32_t end = min(beg + CHUNK, total);
+    uint32_t b = first[t];
+    uint32_t seg = chunk_off[b] + (t - offsets[b] / CHUNK);
+    uint32_t bend = offsets[b + 1];
     Jacobian<F> acc = Jacobian<F>::inf();
     // GLV: indices >= nsplit address the phi(P) table
     auto fetch = [&](uint32_t v) {
@@ -104,13 +110,22 @@ __global__ __launch_bounds__(256) void k_accumulate(const uint32_t* __restrict__
     uint32_t v = sorted[beg];
     Affine<F> p = fetch(v);
     for (uint32_t e = beg; e < end; ++e) {
+        if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
+            store_jac<F>(partials, seg, acc);
+            acc = Jacobian<F>::inf();
+            do {
+                ++b;
+            } while (offsets[b + 1] == e);  // skip empty buckets
+            seg = chunk_off[b];
+            bend = offsets[b + 1];
+        }
         const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
         const Affine<F> pn = fetch(vn);
         acc = jac_madd(acc, (v & 1) ? aff_neg(p) : p);
         v = vn;
         p = pn;
     }
-    store_jac<F>(partials, ch, acc);
+    store_jac<F>(partials, seg, acc);
 }
 
 // ------------------------------------------------------------------------------------
@@ -458,9 +473,9 @@ struct GroupTraits<Fq2> {
 };
 
 struct MsmScratchSizes {
-    size_t dsrc, keys, vals, ranks, sorted, words, tmp, owner, partials, buckets, levelT, levelR, sums, windows, treetmp, phi;
+    size_t dsrc, keys, vals, ranks, sorted, words, tmp, owner, first, partials, buckets, levelT, levelR, sums, windows, treetmp, phi;
     size_t total() const {
-        return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + partials + buckets + levelT + levelR + sums + windows +
+        return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + first + partials + buckets + levelT + levelR + sums + windows +
                2 * treetmp + phi;
     }
 };
@@ -479,6 +494,7 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     z.words = align_up(((size_t)P.TB + 1) * 4);
     z.tmp = align_up(scan_tmp_words(max_chunks > P.TB ? max_chunks : P.TB) * 4);
     z.owner = align_up((size_t)max_chunks * 4);
+    z.first = align_up((NC / CHUNK + 2) * 4);
     z.partials = align_up((size_t)max_chunks * jac);
     z.buckets = align_up((size_t)P.TB * jac);
     size_t lv = 0, maxblk = 1;
@@ -522,6 +538,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint32_t* chunk_off = (uint32_t*)arena.take(z.words);
     uint32_t* tmp = (uint32_t*)arena.take(z.tmp);
     uint32_t* owner = (uint32_t*)arena.take(z.owner);
+    uint32_t* first = (uint32_t*)arena.take(z.first);
     uint8_t* partials = (uint8_t*)arena.take(z.partials);
     uint8_t* buckets = (uint8_t*)arena.take(z.buckets);
     uint8_t* levelT = (uint8_t*)arena.take(z.levelT);
@@ -545,17 +562,18 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     {
         ProfScope ps("msm.sort", st);
         if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) return er;
-        if ((er = launch_chunk_counts(counts, nchunks, TB, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, st)) != MBLS_SUCCESS) return er;
         if ((er = scan_exclusive(nchunks, chunk_off, TB, tmp, st)) != MBLS_SUCCESS) return er;
         if ((er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
-        if ((er = launch_chunk_owner(chunk_off, TB, owner, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_chunk_owner(chunk_off, offsets, TB, owner, first, st)) != MBLS_SUCCESS) return er;
     }
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
         ProfScope ps("msm.accumulate", st);
         // 222 VGPRs -> 2 waves/SIMD; forcing 3 spills 228 B/lane and runs 17% slower (measured)
-        hipLaunchKernelGGL(k_accumulate<F>, dim3((max_chunks + 255) / 256), dim3(256), 0, st, sorted, offsets,
-                           chunk_off, owner, TB, max_chunks, bases, phi, P.glv ? n : 0xffffffffu, partials);
+        const uint32_t threads = (uint32_t)((NC + CHUNK - 1) / CHUNK);
+        hipLaunchKernelGGL(k_accumulate<F>, dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
+                           chunk_off, first, TB, bases, phi, P.glv ? n : 0xffffffffu, partials);
     }
     {
         ProfScope ps("msm.bucket_sum", st);
