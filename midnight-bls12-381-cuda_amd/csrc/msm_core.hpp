@@ -34,6 +34,7 @@
 #include "mbls_common.hpp"
 #include "mbls_curve.hpp"
 #include "mbls_rowfield.hpp"
+#include "mbls_wavepoint.hpp"
 
 namespace mbls {
 
@@ -218,27 +219,48 @@ MBLS_DEV uint32_t row_id() { return (blockIdx.x * blockDim.x + threadIdx.x) >> 4
 // segments); the later, narrower levels run one segment per ROW (row-sliced arithmetic).
 // Single jac_add call site: the loop alternates the R and S updates.
 // ------------------------------------------------------------------------------------
-template <class F, bool ROW>
+// execution modes of the serial phases: one point chain per LANE (scalar arithmetic), per
+// 16-lane ROW (row-sliced), or per WAVE (row-sliced, independent products spread over rows)
+enum : int { MODE_LANE = 0, MODE_ROW = 1, MODE_WAVE = 2 };
+
+template <class F, int MODE>
 struct RedIO;
 template <class F>
-struct RedIO<F, false> {
+struct RedIO<F, MODE_LANE> {
     using J = Jacobian<F>;
     MBLS_DEV static uint32_t id() { return blockIdx.x * blockDim.x + threadIdx.x; }
     MBLS_DEV static J ld(const uint8_t* b, size_t i) { return load_jac<F>(b, i); }
     MBLS_DEV static void st(uint8_t* b, size_t i, const J& v) { store_jac<F>(b, i, v); }
+    MBLS_DEV static J add(const J& a, const J& b) { return jac_add(a, b); }
+    MBLS_DEV static J dbl(const J& a) { return jac_dbl(a); }
 };
 template <class F>
-struct RedIO<F, true> {
+struct RedIO<F, MODE_ROW> {
     using J = RJac<F>;
     MBLS_DEV static uint32_t id() { return row_id(); }
     MBLS_DEV static J ld(const uint8_t* b, size_t i) { return rload_jac<F>(b, i); }
     MBLS_DEV static void st(uint8_t* b, size_t i, const J& v) { rstore_jac<F>(b, i, v); }
+    MBLS_DEV static J add(const J& a, const J& b) { return jac_add(a, b); }
+    MBLS_DEV static J dbl(const J& a) { return jac_dbl(a); }
 };
+template <class F>
+struct RedIO<F, MODE_WAVE> {
+    using J = RJac<F>;
+    MBLS_DEV static uint32_t id() { return (blockIdx.x * blockDim.x + threadIdx.x) >> 6; }
+    MBLS_DEV static J ld(const uint8_t* b, size_t i) { return rload_jac<F>(b, i); }
+    MBLS_DEV static void st(uint8_t* b, size_t i, const J& v) {
+        if (wave::leader_row()) rstore_jac<F>(b, i, v);
+    }
+    MBLS_DEV static J add(const J& a, const J& b) { return wave::jadd(a, b); }
+    MBLS_DEV static J dbl(const J& a) { return wave::jdbl(a); }
+};
+template <int MODE>
+constexpr uint32_t lanes_per_chain() { return MODE == MODE_LANE ? 1u : MODE == MODE_ROW ? 16u : 64u; }
 
-template <class F, bool ROW>
+template <class F, int MODE>
 __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict__ V, uint32_t m_in, uint32_t seg, int Wg,
                                                       int off, uint8_t* __restrict__ T, uint8_t* __restrict__ R) {
-    using IO = RedIO<F, ROW>;
+    using IO = RedIO<F, MODE>;
     using J = typename IO::J;
     const uint32_t m_out = (m_in + seg - 1) / seg;
     const uint32_t tid = IO::id();
@@ -259,7 +281,7 @@ __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict_
         }
         J x = r_step ? Racc : Sacc;
         J y = r_step ? IO::ld(V, (size_t)w * m_in + t) : Racc;
-        J z = jac_add(x, y);
+        J z = IO::add(x, y);
         if (r_step) {
             Racc = z;
         } else {
@@ -296,31 +318,33 @@ __global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V,
     if (r == 0) rstore_jac<F>(out, blockIdx.x, acc);
 }
 
-// G_w = sumT[0] + seg_0*(sumT[1] + seg_1*(sumT[2] + ...)): sums[l * Wg + w]; one row per window
-template <class F>
+// G_w = sumT[0] + seg_0*(sumT[1] + seg_1*(sumT[2] + ...)): sums[l * Wg + w]; one chain per window
+template <class F, int MODE>
 __global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, int Wg, uint64_t seg_logs,
                                 uint8_t* __restrict__ windows) {
-    const int w = (int)row_id();
+    using IO = RedIO<F, MODE>;
+    const int w = (int)IO::id();
     if (w >= Wg) return;
-    RJac<F> acc = rload_jac<F>(sums, (size_t)(levels - 1) * Wg + w);
+    auto acc = IO::ld(sums, (size_t)(levels - 1) * Wg + w);
     for (int l = levels - 2; l >= 0; --l) {
         const int dbls = (int)((seg_logs >> (4 * l)) & 15);
-        for (int k = 0; k < dbls; ++k) acc = jac_dbl(acc);
-        acc = jac_add(acc, rload_jac<F>(sums, (size_t)l * Wg + w));
+        for (int k = 0; k < dbls; ++k) acc = IO::dbl(acc);
+        acc = IO::add(acc, IO::ld(sums, (size_t)l * Wg + w));
     }
-    rstore_jac<F>(windows, w, acc);
+    IO::st(windows, w, acc);
 }
 
-// final fold over window groups: sum_w 2^(c w) G_w  (one row)
-template <class F>
+// final fold over window groups: sum_w 2^(c w) G_w  (one chain)
+template <class F, int MODE>
 __global__ void k_final(const uint8_t* __restrict__ windows, int Wg, int c, uint8_t* __restrict__ result) {
-    if (row_id() != 0) return;
-    RJac<F> acc = rload_jac<F>(windows, Wg - 1);
+    using IO = RedIO<F, MODE>;
+    if (IO::id() != 0) return;
+    auto acc = IO::ld(windows, Wg - 1);
     for (int w = Wg - 2; w >= 0; --w) {
-        for (int k = 0; k < c; ++k) acc = jac_dbl(acc);
-        acc = jac_add(acc, rload_jac<F>(windows, w));
+        for (int k = 0; k < c; ++k) acc = IO::dbl(acc);
+        acc = IO::add(acc, IO::ld(windows, w));
     }
-    rstore_jac<F>(result, 0, acc);
+    IO::st(result, 0, acc);
 }
 
 template <class F>
@@ -397,10 +421,11 @@ __global__ void k_jac_to_icicle(uint8_t* pts, int count) {
 
 template <class F>
 __global__ void k_sum_jac(const uint8_t* pts, int count, uint8_t* out) {
-    if (row_id() != 0) return;
-    RJac<F> acc = RJac<F>::inf();
-    for (int i = 0; i < count; ++i) acc = jac_add(acc, rload_jac<F>(pts, i));
-    rstore_jac<F>(out, 0, acc);
+    using IO = RedIO<F, MODE_WAVE>;
+    if (IO::id() != 0) return;
+    auto acc = RJac<F>::inf();
+    for (int i = 0; i < count; ++i) acc = IO::add(acc, IO::ld(pts, i));
+    IO::st(out, 0, acc);
 }
 
 template <class F>
@@ -480,6 +505,14 @@ struct MsmScratchSizes {
     }
 };
 
+// reduction levels with fewer segments than this run one segment per wave (MBLS_WAVE_MIN tunes)
+inline uint32_t wave_min_chains() {
+    static const uint32_t v = [] {
+        const char* e = getenv("MBLS_WAVE_MIN");
+        return e ? (uint32_t)atoi(e) : 2048u;
+    }();
+    return v;
+}
 inline uint32_t tree_blocks(uint32_t m) { return (m + 16 * TREE_PER_ROW - 1) / (16 * TREE_PER_ROW); }
 
 inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks) {
@@ -603,14 +636,16 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         const uint32_t m_out = (m_in + seg - 1) / seg;
         uint8_t* T = levelT + lvoff * JAC;
         uint8_t* R = levelR + lvoff * JAC;
+        const uint32_t chains = m_out * (uint32_t)P.Wg;
         if (l == 0) {  // one segment per lane
-            const uint32_t threads = m_out * (uint32_t)P.Wg;
-            hipLaunchKernelGGL((k_reduce_level<F, false>), dim3((threads + 255) / 256), dim3(256), 0, st, V, m_in, seg,
-                               P.Wg, 1, T, R);
-        } else {  // one segment per 16-lane row
-            const uint32_t threads = m_out * (uint32_t)P.Wg * 16;
-            hipLaunchKernelGGL((k_reduce_level<F, true>), dim3((threads + 255) / 256), dim3(256), 0, st, V, m_in, seg,
-                               P.Wg, 0, T, R);
+            hipLaunchKernelGGL((k_reduce_level<F, MODE_LANE>), dim3((chains + 255) / 256), dim3(256), 0, st, V, m_in,
+                               seg, P.Wg, 1, T, R);
+        } else if (chains >= wave_min_chains()) {  // many segments: one per 16-lane row
+            hipLaunchKernelGGL((k_reduce_level<F, MODE_ROW>), dim3((chains * 16 + 255) / 256), dim3(256), 0, st, V,
+                               m_in, seg, P.Wg, 0, T, R);
+        } else {  // few segments: one per wave (latency-bound chains)
+            hipLaunchKernelGGL((k_reduce_level<F, MODE_WAVE>), dim3((chains * 64 + 255) / 256), dim3(256), 0, st, V,
+                               m_in, seg, P.Wg, 0, T, R);
         }
         // sum of this level's T per window: tree stages until one point per window
         MBLS_TRY(hipEventRecord(ctx.events[l], st));
@@ -633,11 +668,11 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     }
     MBLS_TRY(hipEventRecord(ctx.events[P.levels], side));
     MBLS_TRY(hipStreamWaitEvent(st, ctx.events[P.levels], 0));
-    hipLaunchKernelGGL(k_window_horner<F>, dim3((P.Wg * 16 + 63) / 64), dim3(64), 0, st, sums, P.levels, P.Wg, P.seg_logs_packed(),
-                       windows);
+    hipLaunchKernelGGL((k_window_horner<F, MODE_WAVE>), dim3(P.Wg), dim3(64), 0, st, sums, P.levels, P.Wg,
+                       P.seg_logs_packed(), windows);
     {
         ProfScope ps("msm.final", st);
-        hipLaunchKernelGGL(k_final<F>, dim3(1), dim3(64), 0, st, windows, P.Wg, P.c, result);
+        hipLaunchKernelGGL((k_final<F, MODE_WAVE>), dim3(1), dim3(64), 0, st, windows, P.Wg, P.c, result);
     }
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
