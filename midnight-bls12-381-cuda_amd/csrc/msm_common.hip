@@ -50,11 +50,25 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, bool allow
         int v = e ? atoi(e) : SEG_LOG;
         return v >= 1 && v <= 6 ? v : SEG_LOG;
     }();
+    // Level 0 runs one segment per lane; a later level with many segments one per row (16),
+    // one with few segments one per wave with shorter segments (MBLS_WSEG_LOG, tuning).
+    static const int wave_log = [] {
+        const char* e = getenv("MBLS_WSEG_LOG");
+        int v = e ? atoi(e) : SEG_LOG;  // measured: 2 and 3 (more, shorter levels) are slower
+        return v >= 1 && v <= 6 ? v : SEG_LOG;
+    }();
     p.levels = 0;
     uint32_t m = p.B;
     while (true) {
         if (p.levels >= MAX_LEVELS) return MBLS_INVALID_ARGUMENT;
-        p.seg_log[p.levels] = (uint8_t)(p.levels == 0 ? SEG0_LOG : row_log);
+        int lg = SEG0_LOG, mode = MODE_LANE;
+        if (p.levels > 0) {
+            const uint32_t row_chains = ((m + (1u << row_log) - 1) >> row_log) * (uint32_t)Wg;
+            mode = row_chains >= wave_min_chains() ? MODE_ROW : MODE_WAVE;
+            lg = mode == MODE_ROW ? row_log : wave_log;
+        }
+        p.seg_log[p.levels] = (uint8_t)lg;
+        p.mode[p.levels] = (uint8_t)mode;
         p.level_m[p.levels++] = m;
         const uint32_t seg = p.seg(p.levels - 1);
         uint32_t mo = (m + seg - 1) / seg;

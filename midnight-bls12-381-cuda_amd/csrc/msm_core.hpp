@@ -55,6 +55,7 @@ struct MsmPlan {
     int levels;                 // bucket-reduction levels
     uint32_t level_m[MAX_LEVELS];  // inputs per window at each level
     uint8_t seg_log[MAX_LEVELS];   // log2 segment length per level
+    uint8_t mode[MAX_LEVELS];      // MODE_LANE / MODE_ROW / MODE_WAVE per level
     uint32_t seg(int l) const { return 1u << seg_log[l]; }
     uint64_t seg_logs_packed() const {  // 4 bits per level, for k_window_horner
         uint64_t v = 0;
@@ -637,10 +638,10 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         uint8_t* T = levelT + lvoff * JAC;
         uint8_t* R = levelR + lvoff * JAC;
         const uint32_t chains = m_out * (uint32_t)P.Wg;
-        if (l == 0) {  // one segment per lane
+        if (P.mode[l] == MODE_LANE) {  // one segment per lane
             hipLaunchKernelGGL((k_reduce_level<F, MODE_LANE>), dim3((chains + 255) / 256), dim3(256), 0, st, V, m_in,
                                seg, P.Wg, 1, T, R);
-        } else if (chains >= wave_min_chains()) {  // many segments: one per 16-lane row
+        } else if (P.mode[l] == MODE_ROW) {  // many segments: one per 16-lane row
             hipLaunchKernelGGL((k_reduce_level<F, MODE_ROW>), dim3((chains * 16 + 255) / 256), dim3(256), 0, st, V,
                                m_in, seg, P.Wg, 0, T, R);
         } else {  // few segments: one per wave (latency-bound chains)
