@@ -92,16 +92,16 @@ struct Fp {
 using Fr = Fp<FrCfg>;
 using Fq = Fp<FqCfg>;
 
+// Carry chains use __builtin_addc / __builtin_subc, which lower to one v_add_co/v_addc
+// (v_sub_co/v_subb) per word; the 64-bit C formulation produced ~3x the instructions
+// (v_mov + v_lshl_add_u64 per word, measured on an Fq add: 148 vs 53 VALU instructions).
+
 // (a - m) with borrow; returns 1 if a < m
 template <class C>
 MBLS_DEV uint32_t sub_mod_raw(uint32_t (&r)[C::N], const uint32_t (&a)[C::N]) {
-    uint32_t borrow = 0;
+    unsigned borrow = 0;
 #pragma unroll
-    for (int i = 0; i < C::N; ++i) {
-        uint64_t d = (uint64_t)a[i] - C::MOD[i] - borrow;
-        r[i] = (uint32_t)d;
-        borrow = (uint32_t)(d >> 63);
-    }
+    for (int i = 0; i < C::N; ++i) r[i] = __builtin_subc(a[i], C::MOD[i], borrow, &borrow);
     return borrow;
 }
 
@@ -117,13 +117,9 @@ MBLS_DEV void reduce_once(Fp<C>& a) {
 template <class C>
 MBLS_DEV Fp<C> operator+(const Fp<C>& a, const Fp<C>& b) {
     Fp<C> r;
-    uint32_t carry = 0;
+    unsigned carry = 0;
 #pragma unroll
-    for (int i = 0; i < C::N; ++i) {
-        uint64_t s = (uint64_t)a.v[i] + b.v[i] + carry;
-        r.v[i] = (uint32_t)s;
-        carry = (uint32_t)(s >> 32);
-    }
+    for (int i = 0; i < C::N; ++i) r.v[i] = __builtin_addc(a.v[i], b.v[i], carry, &carry);
     // both moduli < 2^(32N-1): a+b < 2m fits in N words, carry == 0
     reduce_once(r);
     return r;
@@ -132,22 +128,14 @@ MBLS_DEV Fp<C> operator+(const Fp<C>& a, const Fp<C>& b) {
 template <class C>
 MBLS_DEV Fp<C> operator-(const Fp<C>& a, const Fp<C>& b) {
     Fp<C> r;
-    uint32_t borrow = 0;
+    unsigned borrow = 0;
 #pragma unroll
-    for (int i = 0; i < C::N; ++i) {
-        uint64_t d = (uint64_t)a.v[i] - b.v[i] - borrow;
-        r.v[i] = (uint32_t)d;
-        borrow = (uint32_t)(d >> 63);
-    }
+    for (int i = 0; i < C::N; ++i) r.v[i] = __builtin_subc(a.v[i], b.v[i], borrow, &borrow);
     // add m back if negative (mask form keeps the wave convergent)
-    uint32_t mask = 0u - borrow;
-    uint32_t carry = 0;
+    const uint32_t mask = 0u - borrow;
+    unsigned carry = 0;
 #pragma unroll
-    for (int i = 0; i < C::N; ++i) {
-        uint64_t s = (uint64_t)r.v[i] + (C::MOD[i] & mask) + carry;
-        r.v[i] = (uint32_t)s;
-        carry = (uint32_t)(s >> 32);
-    }
+    for (int i = 0; i < C::N; ++i) r.v[i] = __builtin_addc(r.v[i], C::MOD[i] & mask, carry, &carry);
     return r;
 }
 

@@ -86,8 +86,8 @@ size_t scan_tmp_words(uint32_t m);
 //    one partial per bucket segment it touches (see k_chunk_counts): no idle lanes on the
 //    short last chunk of each bucket.
 // ------------------------------------------------------------------------------------
-template <class F>
-__global__ __launch_bounds__(256) void k_accumulate(const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets,
+template <class F, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ chunk_off,
                                                     const uint32_t* __restrict__ first, uint32_t TB,
                                                     const uint8_t* __restrict__ bases, const uint8_t* __restrict__ phi,
@@ -604,10 +604,17 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
         ProfScope ps("msm.accumulate", st);
-        // 222 VGPRs -> 2 waves/SIMD; forcing 3 spills 228 B/lane and runs 17% slower (measured)
         const uint32_t threads = (uint32_t)((NC + CHUNK - 1) / CHUNK);
-        hipLaunchKernelGGL(k_accumulate<F>, dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
-                           chunk_off, first, TB, bases, phi, P.glv ? n : 0xffffffffu, partials);
+        static const int w3 = [] {
+            const char* e = getenv("MBLS_ACC_W3");
+            return e ? atoi(e) : 1;
+        }();
+        if (std::is_same<F, Fq>::value && w3)
+            hipLaunchKernelGGL((k_accumulate<F, 3>), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
+                               chunk_off, first, TB, bases, phi, P.glv ? n : 0xffffffffu, partials);
+        else
+            hipLaunchKernelGGL((k_accumulate<F, 1>), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
+                               chunk_off, first, TB, bases, phi, P.glv ? n : 0xffffffffu, partials);
     }
     {
         ProfScope ps("msm.bucket_sum", st);
