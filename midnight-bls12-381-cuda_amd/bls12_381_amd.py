@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libbls12_381_mi355x.so")
+# MBLS_LIB: an alternative in-tree build of the same library (A/B tuning runs only)
+LIB_PATH = os.environ.get("MBLS_LIB") or os.path.join(HERE, "lib", "libbls12_381_mi355x.so")
 
 ERRORS = ["SUCCESS", "INVALID_DEVICE", "OUT_OF_MEMORY", "INVALID_POINTER", "ALLOCATION_FAILED",
           "DEALLOCATION_FAILED", "COPY_FAILED", "SYNCHRONIZATION_FAILED", "STREAM_CREATION_FAILED",

@@ -9,6 +9,7 @@
 // schedule, so the constant-time formulas buy nothing on this path.
 #pragma once
 #include "mbls_field.hpp"
+#include "mbls_pairfield.hpp"
 
 namespace mbls {
 
@@ -74,7 +75,7 @@ MBLS_DEV Jacobian<F> jac_add(const Jacobian<F>& p, const Jacobian<F>& q) {
     F V = U1 * I;
     Jacobian<F> r;
     r.x = sqr(R) - J - dbl(V);
-    r.y = R * (V - r.x) - dbl(S1 * J);
+    r.y = mul_sum(R, V - r.x, neg(dbl(S1)), J);
     r.z = (sqr(p.z + q.z) - Z1Z1 - Z2Z2) * H;
     return r;
 }
@@ -100,7 +101,7 @@ MBLS_DEV Jacobian<F> jac_madd(const Jacobian<F>& p, const Affine<F>& q) {
     F V = p.x * I;
     Jacobian<F> r;
     r.x = sqr(R) - J - dbl(V);
-    r.y = R * (V - r.x) - dbl(p.y * J);
+    r.y = mul_sum(R, V - r.x, neg(dbl(p.y)), J);
     r.z = sqr(p.z + H) - Z1Z1 - HH;
     return r;
 }
@@ -159,6 +160,27 @@ struct FieldIO<Fq2> {
         store<FqCfg>(p, v.c0);
         store<FqCfg>(p + 48, v.c1);
     }
+};
+
+// pair-sliced Fq2: same 96-byte storage, lane j moves the 48 bytes of component j
+template <>
+struct FieldIO<PFq2> {
+    static constexpr int BYTES = 96;
+    MBLS_DEV static PFq2 ld(const uint8_t* p) { return {load<FqCfg>(p + (pairdpp::odd() ? 48 : 0))}; }
+    MBLS_DEV static void st(uint8_t* p, const PFq2& v) { store<FqCfg>(p + (pairdpp::odd() ? 48 : 0), v.v); }
+};
+
+// element type of the one-chain-per-thread ("lane") kernels: G1 uses Fq in one lane, G2 the
+// pair-sliced Fq2 in two lanes (mbls_pairfield.hpp)
+template <class F>
+struct LaneOf {
+    using type = F;
+    static constexpr uint32_t LANES = 1;
+};
+template <>
+struct LaneOf<Fq2> {
+    using type = PFq2;
+    static constexpr uint32_t LANES = 2;
 };
 
 template <class F>

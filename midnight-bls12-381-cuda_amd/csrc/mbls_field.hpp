@@ -194,6 +194,24 @@ MBLS_DEV Fp<C> sqr(const Fp<C>& a) {
     return fips::sqr(a);
 }
 
+#ifndef MBLS_LAZY
+#define MBLS_LAZY 1
+#endif
+// a*b + c*d.  Generic form for the row-sliced / extension types; prime-field elements use one
+// shared Montgomery reduction (fips::mul2).
+template <class F>
+MBLS_DEV F mul_sum(const F& a, const F& b, const F& c, const F& d) {
+    return a * b + c * d;
+}
+template <class C>
+MBLS_DEV Fp<C> mul_sum(const Fp<C>& a, const Fp<C>& b, const Fp<C>& c, const Fp<C>& d) {
+#if MBLS_LAZY
+    return fips::mul2(a, b, c, d);
+#else
+    return a * b + c * d;
+#endif
+}
+
 template <class C>
 MBLS_DEV Fp<C> to_mont(const Fp<C>& a) {
     return a * Fp<C>::r2();

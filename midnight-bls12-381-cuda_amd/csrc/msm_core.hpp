@@ -39,7 +39,10 @@
 namespace mbls {
 
 static constexpr uint32_t INVALID_KEY = 0xffffffffu;
-static constexpr int CHUNK = 16;  // max points per accumulation thread
+#ifndef MBLS_CHUNK
+#define MBLS_CHUNK 16
+#endif
+static constexpr int CHUNK = MBLS_CHUNK;  // max points per accumulation thread
 static constexpr int SEG_LOG = 4;   // default segment length 16, levels >= 1 (row-sliced)
 static constexpr int SEG0_LOG = 2;  // level 0 (one segment per lane): short chains, many lanes
 static constexpr int MAX_MSM_LOG = 26;
@@ -92,7 +95,8 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
                                                     const uint32_t* __restrict__ first, uint32_t TB,
                                                     const uint8_t* __restrict__ bases, const uint8_t* __restrict__ phi,
                                                     uint32_t nsplit, uint8_t* __restrict__ partials) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    using L = typename LaneOf<F>::type;
+    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
     const uint32_t total = offsets[TB];
     const uint32_t beg = t * CHUNK;
     if (beg >= total) return;
@@ -100,21 +104,21 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
     uint32_t b = first[t];
     uint32_t seg = chunk_off[b] + (t - offsets[b] / CHUNK);
     uint32_t bend = offsets[b + 1];
-    Jacobian<F> acc = Jacobian<F>::inf();
+    Jacobian<L> acc = Jacobian<L>::inf();
     // GLV: indices >= nsplit address the phi(P) table
     auto fetch = [&](uint32_t v) {
         uint32_t idx = v >> 1;
         const uint8_t* src = idx >= nsplit ? phi : bases;
         idx = idx >= nsplit ? idx - nsplit : idx;
-        return load_affine<F>(src, idx);
+        return load_affine<L>(src, idx);
     };
     // one point ahead: the next random 96/192-byte fetch overlaps this mixed addition
     uint32_t v = sorted[beg];
-    Affine<F> p = fetch(v);
+    Affine<L> p = fetch(v);
     for (uint32_t e = beg; e < end; ++e) {
         if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
-            store_jac<F>(partials, seg, acc);
-            acc = Jacobian<F>::inf();
+            store_jac<L>(partials, seg, acc);
+            acc = Jacobian<L>::inf();
             do {
                 ++b;
             } while (offsets[b + 1] == e);  // skip empty buckets
@@ -122,12 +126,12 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
             bend = offsets[b + 1];
         }
         const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
-        const Affine<F> pn = fetch(vn);
+        const Affine<L> pn = fetch(vn);
         acc = jac_madd(acc, (v & 1) ? aff_neg(p) : p);
         v = vn;
         p = pn;
     }
-    store_jac<F>(partials, seg, acc);
+    store_jac<L>(partials, seg, acc);
 }
 
 // ------------------------------------------------------------------------------------
@@ -144,37 +148,43 @@ __global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ owner, uint32_t TB,
                                                      uint32_t max_chunks, const uint32_t* __restrict__ maxc,
                                                      uint32_t step, uint8_t* __restrict__ partials) {
+    using L = typename LaneOf<F>::type;
+    constexpr uint32_t LN = LaneOf<F>::LANES;
     if (*maxc <= SMALL_MAX || step >= *maxc) return;  // only heavy buckets remain
     const uint32_t total = min(max_chunks, chunk_off[TB]);
     // capped grid, grid-stride: a pass that finds no work costs one small launch
-    for (uint32_t ch = blockIdx.x * blockDim.x + threadIdx.x; ch < total; ch += gridDim.x * blockDim.x) {
+    for (uint32_t ch = (blockIdx.x * blockDim.x + threadIdx.x) / LN; ch < total; ch += gridDim.x * blockDim.x / LN) {
         const uint32_t b = owner[ch];
         const uint32_t j = ch - chunk_off[b];
         const uint32_t cnt = chunk_off[b + 1] - chunk_off[b];
         if (cnt <= SMALL_MAX) continue;  // summed by k_bucket_small
         if (j % (TREE_FANIN * step) != 0 || j + step >= cnt) continue;
-        Jacobian<F> acc = load_jac<F>(partials, ch);
+        Jacobian<L> acc = load_jac<L>(partials, ch);
         for (int g = 1; g < TREE_FANIN; ++g) {
             uint32_t o = j + g * step;
             if (o >= cnt) break;
-            acc = jac_add(acc, load_jac<F>(partials, (size_t)ch + g * step));
+            acc = jac_add(acc, load_jac<L>(partials, (size_t)ch + g * step));
         }
-        store_jac<F>(partials, ch, acc);
+        store_jac<L>(partials, ch, acc);
     }
 }
 
 // common case: one thread per bucket sums its <= SMALL_MAX chunk partials
 template <class F>
-__global__ __launch_bounds__(256) void k_bucket_small(const uint32_t* __restrict__ chunk_off, uint32_t m,
+#ifndef MBLS_BS_MINW
+#define MBLS_BS_MINW 1
+#endif
+__global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32_t* __restrict__ chunk_off, uint32_t m,
                                                       const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
-    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    using L = typename LaneOf<F>::type;
+    uint32_t b = (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
     if (b >= m) return;
     const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
     if (k1 - k0 > SMALL_MAX) return;  // heavy: tree passes + k_bucket_gather
-    Jacobian<F> acc = Jacobian<F>::inf();
-    if (k1 > k0) acc = load_jac<F>(partials, k0);
-    for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<F>(partials, k));
-    store_jac<F>(buckets, b, acc);
+    Jacobian<L> acc = Jacobian<L>::inf();
+    if (k1 > k0) acc = load_jac<L>(partials, k0);
+    for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<L>(partials, k));
+    store_jac<L>(buckets, b, acc);
 }
 
 template <class F>
@@ -228,10 +238,11 @@ template <class F, int MODE>
 struct RedIO;
 template <class F>
 struct RedIO<F, MODE_LANE> {
-    using J = Jacobian<F>;
-    MBLS_DEV static uint32_t id() { return blockIdx.x * blockDim.x + threadIdx.x; }
-    MBLS_DEV static J ld(const uint8_t* b, size_t i) { return load_jac<F>(b, i); }
-    MBLS_DEV static void st(uint8_t* b, size_t i, const J& v) { store_jac<F>(b, i, v); }
+    using L = typename LaneOf<F>::type;
+    using J = Jacobian<L>;
+    MBLS_DEV static uint32_t id() { return (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES; }
+    MBLS_DEV static J ld(const uint8_t* b, size_t i) { return load_jac<L>(b, i); }
+    MBLS_DEV static void st(uint8_t* b, size_t i, const J& v) { store_jac<L>(b, i, v); }
     MBLS_DEV static J add(const J& a, const J& b) { return jac_add(a, b); }
     MBLS_DEV static J dbl(const J& a) { return jac_dbl(a); }
 };
@@ -552,6 +563,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
                         const MsmPlan& P, uint8_t* result, StreamCtx& ctx, hipStream_t st) {
     Arena& arena = ctx.arena;
     constexpr size_t JAC = GroupTraits<F>::JAC, AFF = GroupTraits<F>::AFF;
+    constexpr uint32_t LN = LaneOf<F>::LANES;  // lanes per chain in the lane-mode kernels
     if (n == 0) {
         hipLaunchKernelGGL(k_store_inf<F>, dim3(1), dim3(64), 0, st, result, 1);
         MBLS_TRY(hipGetLastError());
@@ -604,7 +616,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
         ProfScope ps("msm.accumulate", st);
-        const uint32_t threads = (uint32_t)((NC + CHUNK - 1) / CHUNK);
+        const uint32_t threads = (uint32_t)((NC + CHUNK - 1) / CHUNK) * LN;
         static const int w3 = [] {
             const char* e = getenv("MBLS_ACC_W3");
             return e ? atoi(e) : 1;
@@ -620,11 +632,11 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         ProfScope ps("msm.bucket_sum", st);
         // worst case: every contribution of a window group in one bucket
         const uint32_t max_per_bucket = (uint32_t)((P.pts + CHUNK - 1) / CHUNK);
-        hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials,
+        hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB * LN + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials,
                            buckets);
         if (max_per_bucket > SMALL_MAX) {
             for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
-                hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks + 255) / 256, 1024u)), dim3(256), 0, st, chunk_off,
+                hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN + 255) / 256, 1024u)), dim3(256), 0, st, chunk_off,
                                    owner, TB, max_chunks, nchunks + TB, step, partials);
             hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB,
                                nchunks + TB, partials, buckets);
@@ -646,7 +658,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         uint8_t* R = levelR + lvoff * JAC;
         const uint32_t chains = m_out * (uint32_t)P.Wg;
         if (P.mode[l] == MODE_LANE) {  // one segment per lane
-            hipLaunchKernelGGL((k_reduce_level<F, MODE_LANE>), dim3((chains + 255) / 256), dim3(256), 0, st, V, m_in,
+            hipLaunchKernelGGL((k_reduce_level<F, MODE_LANE>), dim3((chains * LN + 255) / 256), dim3(256), 0, st, V, m_in,
                                seg, P.Wg, 1, T, R);
         } else if (P.mode[l] == MODE_ROW) {  // many segments: one per 16-lane row
             hipLaunchKernelGGL((k_reduce_level<F, MODE_ROW>), dim3((chains * 16 + 255) / 256), dim3(256), 0, st, V,
