@@ -168,6 +168,9 @@ eIcicleError bls12_381_field_ntt_cuda(const mbls_fr_t* input, int size, NTTDir d
                                       mbls_fr_t* output);
 eIcicleError bls12_381_field_ntt_init_domain_cuda(const mbls_fr_t* root_of_unity, const NTTInitDomainConfig* config);
 eIcicleError bls12_381_field_ntt_release_domain_cuda(void);
+/* w_(2^logn) of the initialised domain (Montgomery); INVALID_ARGUMENT without a domain or past
+ * its order.  Backs ICICLE's NttGetRouFromDomainImpl (icicle_backend_api.cuh:135-138). */
+eIcicleError bls12_381_ntt_get_rou_from_domain(uint64_t logn, mbls_fr_t* rou);
 
 /* ------------------------------------------------------------------------------------ */
 /* vecops (reference vec_ops.cu:393-524 and :693-840; icicle_field_api.cu:194-334)        */

@@ -65,7 +65,7 @@ EXPORTED = [
     "bls12_381_icicle_g1_msm_precompute_bases", "bls12_381_icicle_g2_msm_precompute_bases",
     "bls12_381_ntt_init_domain_cuda", "bls12_381_ntt_release_domain_cuda", "bls12_381_ntt_cuda",
     "bls12_381_coset_ntt_cuda", "bls12_381_field_ntt_cuda", "bls12_381_field_ntt_init_domain_cuda",
-    "bls12_381_field_ntt_release_domain_cuda",
+    "bls12_381_field_ntt_release_domain_cuda", "bls12_381_ntt_get_rou_from_domain",
     "bls12_381_vector_add", "bls12_381_vector_sub", "bls12_381_vector_mul", "bls12_381_scalar_mul_vec",
     "bls12_381_scalar_add_vec", "vec_add_cuda", "vec_sub_cuda", "vec_mul_cuda", "scalar_mul_vec_cuda",
     "scalar_add_vec_cuda", "vec_sum_cuda", "bls12_381_batch_inv_cuda",
@@ -95,7 +95,7 @@ def lib():
         "bls12_381_ntt_init_domain_cuda": [P, P], "bls12_381_ntt_release_domain_cuda": [],
         "bls12_381_ntt_cuda": [P, i32, i32, P, P], "bls12_381_coset_ntt_cuda": [P, i32, i32, P, P, P],
         "bls12_381_field_ntt_cuda": [P, i32, i32, P, P], "bls12_381_field_ntt_init_domain_cuda": [P, P],
-        "bls12_381_field_ntt_release_domain_cuda": [],
+        "bls12_381_field_ntt_release_domain_cuda": [], "bls12_381_ntt_get_rou_from_domain": [u64, P],
         "bls12_381_vector_add": [P, P, sz, P, P], "bls12_381_vector_sub": [P, P, sz, P, P],
         "bls12_381_vector_mul": [P, P, sz, P, P], "bls12_381_scalar_mul_vec": [P, P, sz, P, P],
         "bls12_381_scalar_add_vec": [P, P, sz, P, P],

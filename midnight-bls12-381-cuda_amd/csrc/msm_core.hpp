@@ -598,12 +598,22 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
+    // side stream: the phi(P) table and the heavy-bucket passes overlap the main chain; the
+    // per-level tree sums of the reduction run there too.  Events [levels+1 ..) fork / join.
+    if ((er = ctx.ensure_side((size_t)P.levels + 5)) != MBLS_SUCCESS) return er;
+    hipStream_t side = ctx.side;
+    hipEvent_t* ev = ctx.events.data() + P.levels + 1;
+    if (P.glv) {
+        MBLS_TRY(hipEventRecord(ev[0], st));
+        MBLS_TRY(hipStreamWaitEvent(side, ev[0], 0));
+        if ((er = launch_glv_table(bases, phi, n, side)) != MBLS_SUCCESS) return er;
+        MBLS_TRY(hipEventRecord(ev[1], side));
+    }
     {
         ProfScope ps("msm.digits", st);
         MBLS_TRY(hipMemsetAsync(counts, 0, (size_t)TB * 4, st));
         er = launch_digits(scalars, scalars_mont, n, P, keys, vals, ranks, counts, dsrc, st);
         if (er != MBLS_SUCCESS) return er;
-        if (P.glv && (er = launch_glv_table(bases, phi, n, st)) != MBLS_SUCCESS) return er;
     }
     {
         ProfScope ps("msm.sort", st);
@@ -616,6 +626,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
         ProfScope ps("msm.accumulate", st);
+        if (P.glv) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
         const uint32_t threads = (uint32_t)((NC + CHUNK - 1) / CHUNK) * LN;
         static const int w3 = [] {
             const char* e = getenv("MBLS_ACC_W3");
@@ -632,22 +643,26 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         ProfScope ps("msm.bucket_sum", st);
         // worst case: every contribution of a window group in one bucket
         const uint32_t max_per_bucket = (uint32_t)((P.pts + CHUNK - 1) / CHUNK);
+        // heavy buckets (> SMALL_MAX chunks; no-op passes for random inputs) on the side stream,
+        // concurrently with the light ones: disjoint partials / buckets
+        if (max_per_bucket > SMALL_MAX) {
+            MBLS_TRY(hipEventRecord(ev[2], st));
+            MBLS_TRY(hipStreamWaitEvent(side, ev[2], 0));
+            for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
+                hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN + 255) / 256, 1024u)), dim3(256), 0, side, chunk_off,
+                                   owner, TB, max_chunks, nchunks + TB, step, partials);
+            hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, side, chunk_off, TB,
+                               nchunks + TB, partials, buckets);
+            MBLS_TRY(hipEventRecord(ev[3], side));
+        }
         hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB * LN + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials,
                            buckets);
-        if (max_per_bucket > SMALL_MAX) {
-            for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
-                hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN + 255) / 256, 1024u)), dim3(256), 0, st, chunk_off,
-                                   owner, TB, max_chunks, nchunks + TB, step, partials);
-            hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, st, chunk_off, TB,
-                               nchunks + TB, partials, buckets);
-        }
+        if (max_per_bucket > SMALL_MAX) MBLS_TRY(hipStreamWaitEvent(st, ev[3], 0));
     }
     ProfScope ps_red("msm.reduce", st);
     // recursive running-sum reduction.  The per-level T tree sums are latency-bound chains off
     // the critical path: they run on the context's side stream, forked after each level and
     // joined before the window Horner.
-    if ((er = ctx.ensure_side((size_t)P.levels + 1)) != MBLS_SUCCESS) return er;
-    hipStream_t side = ctx.side;
     const uint8_t* V = buckets;
     size_t lvoff = 0;
     for (int l = 0; l < P.levels; ++l) {

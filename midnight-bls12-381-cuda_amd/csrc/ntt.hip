@@ -555,4 +555,14 @@ eIcicleError bls12_381_field_ntt_init_domain_cuda(const mbls_fr_t* root_of_unity
 }
 eIcicleError bls12_381_field_ntt_release_domain_cuda(void) { return ntt_release_domain(); }
 
+// ICICLE get_root_of_unity_from_domain (registered as NttGetRouFromDomainImpl,
+// icicle_backend_api.cuh:135-138): w_(2^logn) of the initialised domain, Montgomery form
+eIcicleError bls12_381_ntt_get_rou_from_domain(uint64_t logn, mbls_fr_t* rou) {
+    if (!rou) return MBLS_INVALID_POINTER;
+    std::lock_guard<std::mutex> lk(g_domain_mu);
+    if (!g_domain.tw || logn > (uint64_t)g_domain.order_log) return MBLS_INVALID_ARGUMENT;
+    canonical_omega(rou->limbs, (int)logn);
+    return MBLS_SUCCESS;
+}
+
 }  // extern "C"
