@@ -22,16 +22,21 @@ static int optimal_c(long long n) {
     return 16;
 }
 
-eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, bool allow_glv) {
+eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) {
     int c = cfg->c > 0 ? cfg->c : optimal_c(n);
     if (c < 2 || c > 20) return MBLS_INVALID_ARGUMENT;
     int bits = cfg->bitsize > 0 ? cfg->bitsize : 255;
     if (bits > 256) return MBLS_INVALID_ARGUMENT;
     int F = cfg->precompute_factor > 0 ? cfg->precompute_factor : 1;
-    // GLV (G1, no precomputed table, full-width scalars): two half-width digit streams < 2^127
-    p.glv = allow_glv && F == 1 && bits > 128;
+    // Endomorphism split (no precomputed table, wide scalars):
+    //   G1 GLV: two half-width digit streams, |m| < 2^127;
+    //   G2 psi: four quarter-width streams, |m| < 2^63 (tiled digits only, c <= 16; worth it
+    //   only for wide scalars: plain needs ceil((bits+1)/c) windows of n, psi 4 x ceil(64/c)).
+    p.split = 1;
+    if (endo == 2 && F == 1 && bits > 128) p.split = 2;
+    if (endo == 4 && F == 1 && bits > 192 && c <= 16) p.split = 4;
     // signed digits need one bit of headroom for the top carry
-    int W = p.glv ? (128 + c - 1) / c : (bits + 1 + c - 1) / c;
+    int W = p.split == 2 ? (128 + c - 1) / c : p.split == 4 ? (64 + c - 1) / c : (bits + 1 + c - 1) / c;
     if (F > W) F = W;
     int Wg = (W + F - 1) / F;
     p.c = c;
@@ -40,8 +45,8 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, bool allow
     p.Wg = Wg;
     p.B = 1u << (c - 1);
     p.TB = (uint32_t)Wg * p.B;
-    p.pts = (size_t)n * (p.glv ? 2 : F);  // point indices per window (P_i then phi(P_i))
-    p.contributions = (size_t)n * W * (p.glv ? 2 : 1);
+    p.pts = (size_t)n * (p.split > 1 ? p.split : F);  // point indices (P_i, then the images)
+    p.contributions = (size_t)n * W * p.split;
     if (p.pts >= (1u << 31)) return MBLS_INVALID_ARGUMENT;
     // reduction levels: level 0 has B inputs, level l divides by 2^seg_log[l], the last has
     // one output.  MBLS_ROW_SEG_LOG (tuning) overrides the row-level segment length.
@@ -336,6 +341,112 @@ eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hi
 }
 
 // ------------------------------------------------------------------------------------
+// 1b'. psi split (G2): s == sum_j (-1)^neg_j m_j psi^j(Q) on G2, m_j < 2^63
+//      (oracle/pyref.py psi_decompose).  psi = [z] on G2 and r = x^4 - x^2 + 1 for x = |z|,
+//      so balanced base-x digits d_j (|d_j| <= x/2) plus the carry d_4 folded back with
+//      x^4 == x^2 - 1 give s == sum_j d_j x^j == sum_j (-1)^j d_j z^j.
+//      Point index j*n + i carries psi^j(P_i) (k_psi_table); the digit source per index is
+//      one uint4 in the GLV format (magnitude words 0-1, bit 127 = sign).
+// ------------------------------------------------------------------------------------
+static constexpr uint64_t PSI_X = 0xd201000000010000ull;  // |z| = PSI_XP << 16
+static constexpr uint64_t PSI_XP = 0xd20100000001ull;
+
+// t <- t div |z|, returns t mod |z|  (t: 8 little-endian u32 words).  |z| = 2^16 x' with a
+// 48-bit x', so the division is a 16-bit-digit long division of t >> 16 by x' (every partial
+// remainder * 2^16 + digit fits 64 bits).
+MBLS_DEV uint64_t divmod_x(uint32_t (&t)[8]) {
+    const uint32_t low16 = t[0] & 0xffffu;
+    uint64_t r = 0;
+    uint32_t q[8];
+#pragma unroll
+    for (int w = 7; w >= 0; --w) {
+        const uint32_t uw = (t[w] >> 16) | (w < 7 ? (t[w + 1] << 16) : 0u);  // word w of t >> 16
+        uint64_t cur = (r << 16) | (uw >> 16);
+        const uint64_t qh = cur / PSI_XP;
+        r = cur - qh * PSI_XP;
+        cur = (r << 16) | (uw & 0xffffu);
+        const uint64_t ql = cur / PSI_XP;
+        r = cur - ql * PSI_XP;
+        q[w] = (uint32_t)((qh << 16) | ql);
+    }
+#pragma unroll
+    for (int w = 0; w < 8; ++w) t[w] = q[w];
+    return (r << 16) | low16;
+}
+
+template <bool MONT>
+__global__ __launch_bounds__(256) void k_psi_split(const uint8_t* __restrict__ scalars, uint32_t n,
+                                                   uint4* __restrict__ out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
+    if (MONT) s = from_mont(s);
+    uint32_t t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[k] = s.v[k];
+    int64_t d[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t rem = divmod_x(t);
+        if (rem > (PSI_X >> 1)) {  // balance: rem - x, carry one into the quotient
+            d[j] = -(int64_t)(PSI_X - rem);
+            unsigned c = 1;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t[k] = __builtin_addc(t[k], 0u, c, &c);
+        } else {
+            d[j] = (int64_t)rem;
+        }
+    }
+    const int64_t d4 = (int64_t)t[0];  // s < r < x^4: the fifth digit is 0 or 1
+    d[2] += d4;
+    d[0] -= d4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool neg = (d[j] < 0) != ((j & 1) != 0);  // psi^j = [z^j] = [(-x)^j]
+        const uint64_t m = (uint64_t)(d[j] < 0 ? -d[j] : d[j]);
+        out[(size_t)j * n + i] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), 0u, neg ? 0x80000000u : 0u);
+    }
+}
+
+// psi(x, y) = (conj(x) * CX, conj(y) * CY), CX = (0, CX1) (oracle/pyref.py PSI_CX / PSI_CY),
+// Montgomery limbs; the table holds psi^1..3(P_i) at (j-1)*n + i
+__constant__ uint32_t PSI_CX1_MONT[12] = {0x867545c3u, 0x890dc9e4u, 0x3285a5d5u, 0x2af32253u, 0x309b7e2cu, 0x50880866u,
+                                          0x7e881024u, 0xa20d1b8cu, 0xe2db9068u, 0x14e4f04fu, 0x1564853au, 0x14e56d3fu};
+__constant__ uint32_t PSI_CY0_MONT[12] = {0xa55c9ad1u, 0x3e2f585du, 0x86c18183u, 0x4294213du, 0x8b623732u, 0x382844c8u,
+                                          0x19103e18u, 0x92ad2afdu, 0xac7cf0b9u, 0x1d794e4fu, 0x7d825ec8u, 0x0bd592fcu};
+__constant__ uint32_t PSI_CY1_MONT[12] = {0x5aa30fdau, 0x7bcfa7a2u, 0x2a927e7cu, 0xdc17dec1u, 0x6b4ebef1u, 0x2f088dd8u,
+                                          0xda74d4a7u, 0xd1ca2087u, 0x96cebc1du, 0x2da25966u, 0xbbfd87d2u, 0x0e2b7eedu};
+
+__global__ void k_psi_table(const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi, uint32_t n) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fq cx1;
+    Fq2 cy;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        cx1.v[k] = PSI_CX1_MONT[k];
+        cy.c0.v[k] = PSI_CY0_MONT[k];
+        cy.c1.v[k] = PSI_CY1_MONT[k];
+    }
+    Affine<Fq2> p = load_affine<Fq2>(bases, i);
+    for (int j = 0; j < 3; ++j) {
+        // conj(x) * (CX1 u) = x1 CX1 + x0 CX1 u; identity (0, 0) maps to itself
+        Affine<Fq2> q;
+        q.x.c0 = p.x.c1 * cx1;
+        q.x.c1 = p.x.c0 * cx1;
+        q.y = Fq2{p.y.c0, neg(p.y.c1)} * cy;
+        p = q;
+        store_affine<Fq2>(phi, (size_t)j * n + i, p);
+    }
+}
+
+eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st) {
+    hipLaunchKernelGGL(k_psi_table, dim3((n + 255) / 256), dim3(256), 0, st, bases, phi, n);
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
+}
+
+// ------------------------------------------------------------------------------------
 // 1c. tiled digits (c <= 16): workgroup (tile, window) histograms its tile's digits in LDS
 //     (local rank = LDS atomic return), then flushes the histogram with ONE coalesced
 //     returning global add per bucket (base of this tile in the bucket).  Random-address
@@ -452,7 +563,8 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_tiled(const uint32_t* __r
     }
 }
 
-size_t digits_src_bytes(uint32_t n) { return (size_t)n * 32; }
+// digit sources per scalar: GLV 2 x 16 B, psi 4 x 16 B, plain standard scalars 32 B
+size_t digits_src_bytes(uint32_t n, int split) { return (size_t)n * (split == 4 ? 64 : 32); }
 
 eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* keys,
                            uint32_t* vals, uint32_t* ranks, uint32_t* counts, uint8_t* dsrc, hipStream_t st) {
@@ -460,13 +572,20 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
     if (P.B <= DT_MAX_B) {
         const uint32_t* src;
         uint32_t nidx;
-        if (P.glv) {
+        if (P.split == 2) {
             if (mont)
                 hipLaunchKernelGGL(k_glv_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
             else
                 hipLaunchKernelGGL(k_glv_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
             src = (const uint32_t*)dsrc;
             nidx = 2 * n;
+        } else if (P.split == 4) {
+            if (mont)
+                hipLaunchKernelGGL(k_psi_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+            else
+                hipLaunchKernelGGL(k_psi_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+            src = (const uint32_t*)dsrc;
+            nidx = 4 * n;
         } else {
             if (mont) hipLaunchKernelGGL(k_scalars_std, g, dim3(256), 0, st, scalars, n, dsrc);
             src = (const uint32_t*)(mont ? dsrc : scalars);
@@ -474,7 +593,7 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
         }
         const uint32_t tiles = (nidx + DT_TILE - 1) / DT_TILE;
         dim3 gt(tiles * (uint32_t)P.W);
-        if (P.glv)
+        if (P.split > 1)  // GLV / psi sources share the sign-magnitude uint4 format
             hipLaunchKernelGGL(k_digits_tiled<true>, gt, dim3(DT_THREADS), 0, st, src, nidx, P.c, P.Wg, (uint32_t)P.F,
                                P.B, keys, vals, ranks, counts);
         else
@@ -483,7 +602,8 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
         MBLS_TRY(hipGetLastError());
         return MBLS_SUCCESS;
     }
-    if (P.glv) {
+    if (P.split == 4) return MBLS_INVALID_ARGUMENT;  // make_plan keeps psi to c <= 16
+    if (P.split == 2) {
         if (mont)
             hipLaunchKernelGGL(k_digits_glv<true>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.B, keys, vals, ranks, counts);
         else

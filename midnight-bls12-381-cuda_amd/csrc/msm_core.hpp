@@ -51,9 +51,9 @@ static constexpr int MAX_LEVELS = 16;
 
 struct MsmPlan {
     int c, W, Wg, F;
-    bool glv;                   // G1 endomorphism split (msm_common.hip k_digits_glv)
+    int split;                  // endomorphism split: 1 none, 2 G1 GLV (phi), 4 G2 psi
     uint32_t B, TB;
-    size_t pts;                 // distinct point indices (n, n*F, or 2n with GLV)
+    size_t pts;                 // distinct point indices (n, n*F, or split*n)
     size_t contributions;
     int levels;                 // bucket-reduction levels
     uint32_t level_m[MAX_LEVELS];  // inputs per window at each level
@@ -67,12 +67,13 @@ struct MsmPlan {
     }
 };
 
-eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, bool allow_glv = false);
+// endo: the split the group offers (1 none, 2 G1 GLV, 4 G2 psi); make_plan decides whether to use it
+eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo = 1);
 
 // ---- non-templated launchers (msm_common.hip) ----------------------------------------
 eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* keys,
                            uint32_t* vals, uint32_t* ranks, uint32_t* counts, uint8_t* dsrc, hipStream_t st);
-size_t digits_src_bytes(uint32_t n);
+size_t digits_src_bytes(uint32_t n, int split);
 eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint32_t* tmp, hipStream_t st);
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
                                  hipStream_t st);
@@ -82,6 +83,7 @@ eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offse
                                 uint32_t* first, hipStream_t st);
 eIcicleError launch_scalars_from_mont(uint8_t* s, size_t n, hipStream_t st);
 eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
+eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
 size_t scan_tmp_words(uint32_t m);
 
 // ------------------------------------------------------------------------------------
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
     uint32_t seg = chunk_off[b] + (t - offsets[b] / CHUNK);
     uint32_t bend = offsets[b + 1];
     Jacobian<L> acc = Jacobian<L>::inf();
-    // GLV: indices >= nsplit address the phi(P) table
+    // endomorphism split: indices >= nsplit address the image table (phi(P) / psi^j(P))
     auto fetch = [&](uint32_t v) {
         uint32_t idx = v >> 1;
         const uint8_t* src = idx >= nsplit ? phi : bases;
@@ -529,12 +531,12 @@ inline uint32_t tree_blocks(uint32_t m) { return (m + 16 * TREE_PER_ROW - 1) / (
 
 inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks) {
     MsmScratchSizes z;
-    z.phi = P.glv ? align_up(P.pts / 2 * aff) : 0;
+    z.phi = P.split > 1 ? align_up(P.pts / P.split * (P.split - 1) * aff) : 0;
     const size_t NC = P.contributions;
     z.keys = align_up(NC * 4);
     z.vals = align_up(NC * 4);
     z.ranks = align_up(NC * 4);
-    z.dsrc = align_up(digits_src_bytes((uint32_t)(P.glv ? P.pts / 2 : P.pts / P.F)));
+    z.dsrc = align_up(digits_src_bytes((uint32_t)(P.split > 1 ? P.pts / P.split : P.pts / P.F), P.split));
     z.sorted = align_up(NC * 4);
     z.words = align_up(((size_t)P.TB + 1) * 4);
     z.tmp = align_up(scan_tmp_words(max_chunks > P.TB ? max_chunks : P.TB) * 4);
@@ -593,8 +595,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint8_t* windows = (uint8_t*)arena.take(z.windows);
     uint8_t* tree_a = (uint8_t*)arena.take(z.treetmp);
     uint8_t* tree_b = (uint8_t*)arena.take(z.treetmp);
-    uint8_t* phi = P.glv ? (uint8_t*)arena.take(z.phi) : nullptr;
-    if (!tree_b || (P.glv && !phi)) return MBLS_ALLOCATION_FAILED;
+    uint8_t* phi = P.split > 1 ? (uint8_t*)arena.take(z.phi) : nullptr;
+    if (!tree_b || (P.split > 1 && !phi)) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
@@ -603,10 +605,11 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     if ((er = ctx.ensure_side((size_t)P.levels + 5)) != MBLS_SUCCESS) return er;
     hipStream_t side = ctx.side;
     hipEvent_t* ev = ctx.events.data() + P.levels + 1;
-    if (P.glv) {
+    if (P.split > 1) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
         MBLS_TRY(hipEventRecord(ev[0], st));
         MBLS_TRY(hipStreamWaitEvent(side, ev[0], 0));
-        if ((er = launch_glv_table(bases, phi, n, side)) != MBLS_SUCCESS) return er;
+        er = P.split == 2 ? launch_glv_table(bases, phi, n, side) : launch_psi_table(bases, phi, n, side);
+        if (er != MBLS_SUCCESS) return er;
         MBLS_TRY(hipEventRecord(ev[1], side));
     }
     {
@@ -626,7 +629,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
         ProfScope ps("msm.accumulate", st);
-        if (P.glv) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
+        if (P.split > 1) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
         const uint32_t threads = (uint32_t)((NC + CHUNK - 1) / CHUNK) * LN;
         static const int w3 = [] {
             const char* e = getenv("MBLS_ACC_W3");
@@ -634,10 +637,10 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         }();
         if (std::is_same<F, Fq>::value && w3)
             hipLaunchKernelGGL((k_accumulate<F, 3>), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
-                               chunk_off, first, TB, bases, phi, P.glv ? n : 0xffffffffu, partials);
+                               chunk_off, first, TB, bases, phi, P.split > 1 ? n : 0xffffffffu, partials);
         else
             hipLaunchKernelGGL((k_accumulate<F, 1>), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
-                               chunk_off, first, TB, bases, phi, P.glv ? n : 0xffffffffu, partials);
+                               chunk_off, first, TB, bases, phi, P.split > 1 ? n : 0xffffffffu, partials);
     }
     {
         ProfScope ps("msm.bucket_sum", st);
@@ -726,7 +729,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     hipStream_t st = static_cast<hipStream_t>(cfg->stream);
     const int batch = icicle_semantics ? (cfg->batch_size > 0 ? cfg->batch_size : 1) : 1;
     MsmPlan P;
-    eIcicleError er = make_plan(msm_size > 0 ? msm_size : 1, cfg, P, std::is_same<F, Fq>::value);
+    eIcicleError er = make_plan(msm_size > 0 ? msm_size : 1, cfg, P, std::is_same<F, Fq>::value ? 2 : 4);
     if (er != MBLS_SUCCESS) return er;
     const bool scal_mont = icicle_semantics ? cfg->are_scalars_montgomery_form : false;
     const bool pts_mont = icicle_semantics ? cfg->are_points_montgomery_form : true;

@@ -352,6 +352,59 @@ def glv_decompose(s: int):
     return m1, neg1, m2, neg2
 
 
+# --------------------------------------------------------------------------------------
+# psi (untwist-Frobenius-twist) split used by the G2 MSM kernel (k_psi_split).  Not a
+# reference algorithm (the reference G2 MSM runs 16 plain windows); the MSM result is unchanged.
+# psi(x, y) = (conj(x) * PSI_CX, conj(y) * PSI_CY) with PSI_CX = (1+u)^-((p-1)/3),
+# PSI_CY = (1+u)^-((p-1)/2); on G2 psi = [z] (z = BLS_Z), and r = x^4 - x^2 + 1 for x = |z|.
+# --------------------------------------------------------------------------------------
+PSI_X = -BLS_Z  # |z| = 0xd201000000010000
+
+
+def _f2_pow(a, e):
+    acc, b = (1, 0), a
+    while e:
+        if e & 1:
+            acc = f2_mul(acc, b)
+        b = f2_mul(b, b)
+        e >>= 1
+    return acc
+
+
+PSI_CX = f2_inv(_f2_pow((1, 1), (P - 1) // 3))
+PSI_CY = f2_inv(_f2_pow((1, 1), (P - 1) // 2))
+
+
+def psi(pt):
+    if pt is None:
+        return None
+    (x0, x1), (y0, y1) = pt
+    return (f2_mul((x0, (-x1) % P), PSI_CX), f2_mul((y0, (-y1) % P), PSI_CY))
+
+
+def psi_decompose(s: int):
+    """[(mag_j, neg_j)] for j = 0..3 with s * Q == sum_j (-1)^neg_j mag_j psi^j(Q) on G2 and
+    mag_j < 2^63, following the kernel step by step: balanced base-x digits d_j (|d_j| <= x/2),
+    then the carry d_4 folded back with x^4 == x^2 - 1 (mod r); psi = [z] = [-x] flips the
+    sign of the odd digits."""
+    x = PSI_X
+    t = s % R
+    d = []
+    for _ in range(4):
+        t, rem = divmod(t, x)
+        if rem > x // 2:
+            rem -= x
+            t += 1
+        d.append(rem)
+    d[2] += t
+    d[0] -= t
+    out = []
+    for j, dj in enumerate(d):
+        neg = (dj < 0) != (j % 2 == 1)
+        out.append((abs(dj), neg))
+    return out
+
+
 def rng(seed: int) -> random.Random:
     return random.Random(seed)
 

@@ -151,3 +151,13 @@ def glv_edge_scalars():
            (h + 1) * lam, h * lam + h, h * lam + h + 1, (h + 1) * lam + h + 1, (h + 2) * lam - 1, (lam + 1) * lam - 1,
            lam * lam + lam - 1, (1 << 254), (1 << 255) - 1]
     return [s % pyref.R for s in out]
+
+
+def psi_edge_scalars():
+    """scalars on the G2 psi split's boundaries: base-|z| digits at 0, x/2, x/2 + 1, x - 1, the
+    folded fifth digit (s >= x^4 - ... near r), and powers of x"""
+    x, h = pyref.PSI_X, pyref.PSI_X >> 1
+    out = [0, 1, 2, pyref.R - 1, pyref.R - 2, h, h + 1, x - 1, x, x + 1, x * x, x ** 3, x ** 3 - 1,
+           h * (1 + x + x * x + x ** 3), (h + 1) * (1 + x + x * x + x ** 3), (x - 1) * (1 + x + x * x),
+           pyref.R - x ** 3, pyref.R - h * x ** 3, (1 << 254), (1 << 255) - 1]
+    return [s % pyref.R for s in out]

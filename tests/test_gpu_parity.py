@@ -428,6 +428,31 @@ def test_msm_glv_split_boundaries(amd, gh):
     assert gh.decode_icicle("g1", r[0]) == ref
 
 
+def test_msm_psi_split_boundaries(amd, gh):
+    """G2 runs the psi split (psi = [z], four quarter-width digit streams): scalars on its
+    balancing boundaries, full-width and <= 192-bit (bitsize 192 keeps the plain path) against
+    the oracle, through both entry points"""
+    import torch
+    edge = H.psi_edge_scalars()
+    g = pr.rng(22)
+    sc = edge + [g.randrange(pr.R) for _ in range(48 - len(edge))]
+    n = len(sc)
+    b = torch.zeros((n, 24), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g2", b, 78)
+    bn = amd.to_numpy_u64(b)
+    s = H.ints_to_limbs(sc, 4)
+    ref = H.g2_from_affine_mont(H.oracle_msm("g2", s, bn))
+    for c in (0, 5, 13, 16):
+        r = amd.msm("g2", s, bn, c=c, n=n)
+        assert gh.decode_icicle("g2", r[0]) == ref, c
+    r = amd.msm("g2", s, bn, icicle=False, n=n)
+    assert gh.decode_jacobian_mont("g2", r[0]) == ref
+    small = H.ints_to_limbs([x % (1 << 192) for x in sc], 4)
+    ref = H.g2_from_affine_mont(H.oracle_msm("g2", small, bn))
+    r = amd.msm("g2", small, bn, bitsize=192, n=n)
+    assert gh.decode_icicle("g2", r[0]) == ref
+
+
 @pytest.mark.slow
 def test_msm_g1_2_24_bit_exact(amd, gh):
     """north-star size: G1 MSM of 2^24 points (BASELINE config #4 total size, single GPU) equals
