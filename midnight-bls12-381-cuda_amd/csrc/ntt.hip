@@ -74,10 +74,40 @@ __global__ void k_twiddles(uint8_t* table, Fr w, int L, uint32_t count) {
     store<FrCfg>(table + 32 * (size_t)g, acc);
 }
 
+// Lazy butterflies: between the first load and the last store of a transform, values live in
+// [0, 2r) (2r < 2^256).  b*w with b < 2r and a canonical twiddle w < r is < r*R, so the
+// Montgomery product needs no final subtraction (fips::mul<C, false>); a + t and a - t are
+// brought back into [0, 2r) with one conditional 2r correction each (same cost as the
+// canonical add / sub).  The last pass stores canonical values.
+__constant__ uint32_t NTT_TWO_R[8] = {0x00000002u, 0xfffffffeu, 0xfffcb7fdu, 0xa77b4805u,
+                                      0x1343b00au, 0x6673b010u, 0x533afa90u, 0xe7db4ea6u};
+MBLS_DEV Fr add_2r(const Fr& a, const Fr& b) {
+    Fr s, d;
+    unsigned c = 0, br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d.v[i] = __builtin_subc(s.v[i], NTT_TWO_R[i], br, &br);
+    const bool keep = !c && br;  // a + b < 2r
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s.v[i] = keep ? s.v[i] : d.v[i];
+    return s;
+}
+MBLS_DEV Fr sub_2r(const Fr& a, const Fr& b) {
+    Fr d;
+    unsigned br = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+    const uint32_t mask = 0u - br;  // a < b: add 2r (mod 2^256)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d.v[i] = __builtin_addc(d.v[i], NTT_TWO_R[i] & mask, c, &c);
+    return d;
+}
+
 // One pass of up to NTT_TILE_LOG DIT stages.
 //   FIRST: stages 1..L with the bit-reversal gather from `in`; else stages s0+1..s0+L in place.
-//   SCALE: multiply outputs by `scale` (inverse n^-1) on store.
-template <bool FIRST, bool SCALE>
+//   LAST:  store canonical values; SCALE (inverse, implies LAST): multiply them by n^-1.
+template <bool FIRST, bool LAST, bool SCALE>
 __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ out, const uint8_t* __restrict__ in,
                                                           const uint8_t* __restrict__ tw, int log_n, int s0, int L,
                                                           int logC, Fr scale) {
@@ -134,10 +164,10 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ 
             if (l > 1 || !FIRST) {
                 size_t jj = ((size_t)j << s0) + (FIRST ? 0 : lo_base + c);
                 Fr w = load<FrCfg>(tw + 32 * ((((size_t)1 << (s - 1)) - 1) + jj));
-                b = b * w;
+                b = fips::mul<FrCfg, false>(b, w);
             }
-            store<FrCfg>(lds + 32 * (t0 * C + c), a + b);
-            store<FrCfg>(lds + 32 * (t1 * C + c), a - b);
+            store<FrCfg>(lds + 32 * (t0 * C + c), add_2r(a, b));
+            store<FrCfg>(lds + 32 * (t1 * C + c), sub_2r(a, b));
         }
         __syncthreads();
     }
@@ -151,7 +181,8 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ 
             int p = e & (rows - 1), c = e >> L;
             size_t blk = bitrev((uint32_t)(c0 + c), colbits);
             Fr v = load<FrCfg>(lds + 32 * (p * C + c));
-            if (SCALE) v = v * scale;
+            if (SCALE) v = v * scale;  // v < 2r, scale < r: the reduced product is canonical
+            else if (LAST) reduce_once(v);
             store<FrCfg>(out + 32 * (pbase + (blk << L) + p), v);
         }
     } else {
@@ -162,6 +193,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ 
             int c = e & (C - 1), t = e >> logC;
             Fr v = load<FrCfg>(lds + 32 * e);
             if (SCALE) v = v * scale;
+            else if (LAST) reduce_once(v);
             store<FrCfg>(out + 32 * (pbase + (hi << (s0 + L)) + ((size_t)t << s0) + lo0 + c), v);
         }
     }
@@ -341,13 +373,17 @@ eIcicleError ntt_device(uint8_t* out, const uint8_t* in, int log_n, bool inverse
         if (tiles > 0x7fffffff) return MBLS_INVALID_ARGUMENT;
         dim3 grid((unsigned)tiles), blk(NTT_THREADS);
         if (first && last && inverse)
-            hipLaunchKernelGGL((k_ntt_pass<true, true>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
+            hipLaunchKernelGGL((k_ntt_pass<true, true, true>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
+        else if (first && last)
+            hipLaunchKernelGGL((k_ntt_pass<true, true, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
         else if (first)
-            hipLaunchKernelGGL((k_ntt_pass<true, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
+            hipLaunchKernelGGL((k_ntt_pass<true, false, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
         else if (last && inverse)
-            hipLaunchKernelGGL((k_ntt_pass<false, true>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
+            hipLaunchKernelGGL((k_ntt_pass<false, true, true>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
+        else if (last)
+            hipLaunchKernelGGL((k_ntt_pass<false, true, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
         else
-            hipLaunchKernelGGL((k_ntt_pass<false, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
+            hipLaunchKernelGGL((k_ntt_pass<false, false, false>), grid, blk, 0, st, out, in, tw, log_n, s0, L, logC, scale);
         MBLS_TRY(hipGetLastError());
         s0 += L;
     }
