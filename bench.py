@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-mix", action="store_true", help="skip the G2 MSM + batched NTT overlap leg (config #5)")
     ap.add_argument("--mix-batch", type=int, default=4, help="NTT polynomials in the config #5 batch")
+    ap.add_argument("--msm-batch", type=int, default=8, help="members of the batched-MSM leg (0: skip)")
     return ap.parse_args()
 
 
@@ -111,6 +112,34 @@ def main():
     msm_time = float(dt_t.item())
     ms_per_step = msm_time / args.steps * 1e3
     msm_per_sec = world * args.steps / msm_time
+
+    # batched MSMs (ICICLE batch_size, shared device bases, device results): members pipelined
+    # on two streams so each member's latency-bound reduction overlaps the next accumulation
+    batch_leg = None
+    if args.msm_batch > 1:
+        B = args.msm_batch
+        sb = torch.zeros((B * n, 4), dtype=torch.int64, device=dev)
+        amd.gen_scalars(sb, 0x5EED0033 + rank, montgomery=True, stream=stream)
+        rb = torch.zeros((B, 18), dtype=torch.int64, device=dev)
+
+        def batch_step():
+            amd.msm("g1", sb, bases, icicle=True, scalars_mont=True, batch=B, out=rb, stream=stream,
+                    is_async=True, n=n)
+
+        batch_step()
+        barrier_sync()
+        reps = max(2, args.steps // 4)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            batch_step()
+        barrier_sync()
+        bdt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(bdt, op=dist.ReduceOp.MAX)
+        batch_leg = {"batch": B, "reps": reps, "ms_per_batch": round(float(bdt.item()) / reps * 1e3, 3),
+                     "msm_per_sec": round(world * B * reps / float(bdt.item()), 3),
+                     "note": "ICICLE batch_size (core/msm.rs msm_batch_with_device_bases), members pipelined on two HIP streams"}
+        del sb
 
     # live per-stage timing (HIP events on this stream) for the roofline
     amd.profile(True)
@@ -210,6 +239,7 @@ def main():
                          "traffic": pmc_traffic("k_accumulate"),
                          "traffic_source": "profiles/r01/pmc_summary.json (bytes per launch)",
                          "note": "VALU-bound (v_mad_u64_u32); HBM fraction reported as the contract asks"},
+            "msm_batch": batch_leg,
             "ntt20_roundtrip_ms": round(ntt20_rt_ms, 4),
             "ntt20_roundtrip_exact": ntt20_exact,
             "mix_g2msm_batched_ntt": mix,

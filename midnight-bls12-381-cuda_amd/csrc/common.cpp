@@ -88,6 +88,14 @@ eIcicleError StreamCtx::ensure_side(size_t nevents) {
     return MBLS_SUCCESS;
 }
 
+eIcicleError StreamCtx::ensure_pipe() {
+    for (int k = 0; k < 2; ++k)
+        if (!pipe[k]) MBLS_TRY(hipStreamCreateWithFlags(&pipe[k], hipStreamNonBlocking));
+    for (int k = 0; k < 3; ++k)
+        if (!pipe_ev[k]) MBLS_TRY(hipEventCreateWithFlags(&pipe_ev[k], hipEventDisableTiming));
+    return MBLS_SUCCESS;
+}
+
 bool is_device_pointer(const void* p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {

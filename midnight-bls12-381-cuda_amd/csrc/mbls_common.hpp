@@ -55,8 +55,14 @@ struct StreamCtx {
     // stream-ordered operation
     hipStream_t side = nullptr;
     std::vector<hipEvent_t> events;
+    // batch pipeline: two private streams (each with its own StreamCtx / arena) that run
+    // alternate batch members, so one member's latency-bound tail overlaps the next member's
+    // accumulation; pipe_ev[0] forks them from this stream, pipe_ev[1..2] join them back
+    hipStream_t pipe[2] = {nullptr, nullptr};
+    hipEvent_t pipe_ev[3] = {nullptr, nullptr, nullptr};
     explicit StreamCtx(hipStream_t s) : arena(s) {}
     eIcicleError ensure_side(size_t nevents);
+    eIcicleError ensure_pipe();
 };
 StreamCtx& stream_ctx(hipStream_t s);
 

@@ -519,6 +519,16 @@ struct MsmScratchSizes {
     }
 };
 
+// batch members on two pipeline streams (default; MBLS_BATCH_PIPE=0 runs them in order on the
+// caller's stream)
+inline bool batch_pipeline() {
+    static const bool v = [] {
+        const char* e = getenv("MBLS_BATCH_PIPE");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 // reduction levels with fewer segments than this run one segment per wave (MBLS_WAVE_MIN tunes)
 inline uint32_t wave_min_chains() {
     static const uint32_t v = [] {
@@ -560,9 +570,11 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
 
 // Core MSM on device operands: scalars (standard or Montgomery), bases Montgomery affine
 // (F*n entries when precomputed); result: one Jacobian Montgomery point on device.
+// use_side = false runs everything on `st` (pipelined batch members: their overlap comes from
+// the two pipeline streams, and fewer streams than the 4 hardware queues keeps them concurrent)
 template <class F>
 eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t* bases, uint32_t n,
-                        const MsmPlan& P, uint8_t* result, StreamCtx& ctx, hipStream_t st) {
+                        const MsmPlan& P, uint8_t* result, StreamCtx& ctx, hipStream_t st, bool use_side = true) {
     Arena& arena = ctx.arena;
     constexpr size_t JAC = GroupTraits<F>::JAC, AFF = GroupTraits<F>::AFF;
     constexpr uint32_t LN = LaneOf<F>::LANES;  // lanes per chain in the lane-mode kernels
@@ -603,7 +615,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     // side stream: the phi(P) table and the heavy-bucket passes overlap the main chain; the
     // per-level tree sums of the reduction run there too.  Events [levels+1 ..) fork / join.
     if ((er = ctx.ensure_side((size_t)P.levels + 5)) != MBLS_SUCCESS) return er;
-    hipStream_t side = ctx.side;
+    hipStream_t side = use_side ? ctx.side : st;
     hipEvent_t* ev = ctx.events.data() + P.levels + 1;
     if (P.split > 1) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
         MBLS_TRY(hipEventRecord(ev[0], st));
@@ -769,13 +781,39 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
         d_b = static_cast<const uint8_t*>(t);
     }
     uint8_t* d_r = static_cast<uint8_t*>(A.take(JAC * (size_t)batch));
-    const size_t mark = A.mark();
-    for (int b = 0; b < batch; ++b) {
-        A.rewind(mark);  // scratch reused across the batch (stream-ordered)
-        const uint8_t* sb = d_s + (size_t)b * n * 32;
-        const uint8_t* bb = d_b + (shared ? 0 : (size_t)b * nbases_per * AFF);
-        er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, ctx, st);
-        if (er != MBLS_SUCCESS) return er;
+    if (batch >= 2 && batch_pipeline()) {
+        // members alternate between the two pipeline streams (own scratch each); member b's
+        // reduction tail runs while member b+1 accumulates on the other stream
+        if ((er = ctx.ensure_pipe()) != MBLS_SUCCESS) return er;
+        MBLS_TRY(hipEventRecord(ctx.pipe_ev[0], st));
+        for (int k = 0; k < 2; ++k) MBLS_TRY(hipStreamWaitEvent(ctx.pipe[k], ctx.pipe_ev[0], 0));
+        for (int b = 0; b < batch; ++b) {
+            hipStream_t ps = ctx.pipe[b & 1];
+            StreamCtx& pc = stream_ctx(ps);
+            std::lock_guard<std::mutex> plk(pc.mu);
+            if (b < 2) {
+                pc.arena.reset();
+                if ((er = pc.arena.reserve(scratch + 4096)) != MBLS_SUCCESS) return er;
+            }
+            pc.arena.reset();  // reuse is ordered on ps: member b-2 used it before
+            const uint8_t* sb = d_s + (size_t)b * n * 32;
+            const uint8_t* bb = d_b + (shared ? 0 : (size_t)b * nbases_per * AFF);
+            er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, pc, ps, false);
+            if (er != MBLS_SUCCESS) return er;
+        }
+        for (int k = 0; k < 2; ++k) {
+            MBLS_TRY(hipEventRecord(ctx.pipe_ev[1 + k], ctx.pipe[k]));
+            MBLS_TRY(hipStreamWaitEvent(st, ctx.pipe_ev[1 + k], 0));
+        }
+    } else {
+        const size_t mark = A.mark();
+        for (int b = 0; b < batch; ++b) {
+            A.rewind(mark);  // scratch reused across the batch (stream-ordered)
+            const uint8_t* sb = d_s + (size_t)b * n * 32;
+            const uint8_t* bb = d_b + (shared ? 0 : (size_t)b * nbases_per * AFF);
+            er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, ctx, st);
+            if (er != MBLS_SUCCESS) return er;
+        }
     }
     if (icicle_semantics) {
         hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch * 16 + 63) / 64), dim3(64), 0, st, d_r, batch);

@@ -389,6 +389,29 @@ def test_msm_batch(amd, gh):
     assert cases
 
 
+@pytest.mark.parametrize("group,shared", [("g1", True), ("g1", False), ("g2", True)])
+def test_msm_batch_pipelined_device(amd, gh, group, shared):
+    """batch members run on two pipeline streams (one member's tail overlaps the next one's
+    accumulation): each member equals the single-MSM result (itself pinned to the oracle),
+    device-resident operands, odd batch size, shared and per-member bases"""
+    import torch
+    n, batch = 1 << 12, 5
+    w = 12 if group == "g1" else 24
+    s = torch.zeros((batch * n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED00B0, montgomery=True)
+    nb = n if shared else n * batch
+    b = torch.zeros((nb, w), dtype=torch.int64, device="cuda")
+    amd.gen_bases(group, b, 0x5EED00B1)
+    out = torch.zeros((batch, w * 3 // 2), dtype=torch.int64, device="cuda")
+    amd.msm(group, s, b, scalars_mont=True, batch=batch, shared_bases=shared, out=out, n=n)
+    torch.cuda.synchronize()
+    got = amd.to_numpy_u64(out)
+    for k in range(batch):
+        bk = b if shared else b[k * n:(k + 1) * n]
+        one = amd.msm(group, s[k * n:(k + 1) * n], bk, scalars_mont=True, n=n)
+        assert gh.decode_icicle(group, got[k]) == gh.decode_icicle(group, one[0]), k
+
+
 def test_msm_sum_jacobian_and_convert(amd, gh):
     import torch
     # partial results of a split MSM summed on device == full MSM (the multi-GPU reduction)
