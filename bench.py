@@ -247,7 +247,7 @@ def main():
                              "achieved": round(ntt_ach, 2) if ntt_ach else None, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(ntt_ach / HBM_PEAK_GBS, 5) if ntt_ach else None,
                              "traffic": ntt_traffic(args.ntt_log),
-                             "traffic_source": "profiles/r01/pmc_summary.json (first + later passes)",
+                             "traffic_source": "profiles/r01/pmc_summary.json (first + middle + last pass)",
                              "pass_ms": round(ntt_pass_ms, 4) if ntt_pass_ms else None},
             "cpu_baseline": cpu,
         }
@@ -257,11 +257,12 @@ def main():
 
 
 def ntt_traffic(log_n):
-    """HBM bytes of one 2^22 transform: first pass + (passes - 1) later passes (pmc_probe sizes)"""
+    """HBM bytes of one forward 2^22 transform: first + middle + last pass (pmc_probe sizes)"""
     if log_n != 22:
         return None
-    first, later = pmc_traffic("k_ntt_pass<true, false>"), pmc_traffic("k_ntt_pass<false, false>")
-    return None if first is None or later is None else first + 2 * later
+    parts = [pmc_traffic(k) for k in ("k_ntt_pass<true, false, false>", "k_ntt_pass<false, false, false>",
+                                      "k_ntt_pass<false, true, false>")]
+    return None if any(p is None for p in parts) else sum(parts)
 
 
 def mix_leg(args, amd, torch, dev, rank):

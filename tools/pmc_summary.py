@@ -25,7 +25,8 @@ def load(d, counter):
 
 
 def short(name):
-    for key in ("k_accumulate", "k_ntt_pass<true, false>", "k_ntt_pass<false, false>", "k_ntt_pass<false, true>",
+    for key in ("k_accumulate", "k_ntt_pass<true, false, false>", "k_ntt_pass<false, false, false>",
+                "k_ntt_pass<false, true, false>", "k_ntt_pass<false, true, true>",
                 "k_scatter", "k_digits_tiled", "k_bucket_small", "k_reduce_level", "k_glv_table", "k_vecop"):
         if key.replace(" ", "") in name.replace(" ", ""):
             return key
