@@ -312,10 +312,9 @@ __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict_
 // 16 rows sums `per_row` consecutive points, then a 4-level LDS tree.  out[w*nblk + b].
 static constexpr int TREE_PER_ROW = 8;
 template <class F>
-__global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V, uint32_t m, uint32_t nblk,
-                                                  uint8_t* __restrict__ out) {
+MBLS_DEV void tree_sum_block(const uint8_t* __restrict__ V, uint32_t m, uint32_t w, uint32_t blk,
+                             uint8_t* __restrict__ out, uint32_t out_idx) {
     __shared__ __attribute__((aligned(16))) uint8_t sh[16 * 3 * sizeof(F)];
-    const uint32_t w = blockIdx.x / nblk, blk = blockIdx.x % nblk;
     const uint32_t r = threadIdx.x >> 4;  // row in block
     RJac<F> acc = RJac<F>::inf();
     const uint32_t k0 = (blk * 16 + r) * TREE_PER_ROW;
@@ -329,7 +328,28 @@ __global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V,
         }
         __syncthreads();
     }
-    if (r == 0) rstore_jac<F>(out, blockIdx.x, acc);
+    if (r == 0) rstore_jac<F>(out, out_idx, acc);
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V, uint32_t m, uint32_t nblk,
+                                                  uint8_t* __restrict__ out) {
+    tree_sum_block<F>(V, m, blockIdx.x / nblk, blockIdx.x % nblk, out, blockIdx.x);
+}
+
+// the narrow levels' T sums (<= one tree block per window each), all in one launch after the
+// last level: block (job, window).  Forked per level they serialised on the side stream
+// (~90 us each) behind the main chain.
+static constexpr uint32_t TREE_BLOCK_POINTS = 16 * TREE_PER_ROW;
+struct TreeJobs {
+    const uint8_t* V[MAX_LEVELS];
+    uint8_t* out[MAX_LEVELS];
+    uint32_t m[MAX_LEVELS];
+};
+template <class F>
+__global__ __launch_bounds__(256) void k_tree_sum_jobs(TreeJobs jobs, int Wg) {
+    const uint32_t j = blockIdx.x / Wg, w = blockIdx.x % Wg;
+    tree_sum_block<F>(jobs.V[j], jobs.m[j], w, 0, jobs.out[j], w);
 }
 
 // G_w = sumT[0] + seg_0*(sumT[1] + seg_1*(sumT[2] + ...)): sums[l * Wg + w]; one chain per window
@@ -519,6 +539,16 @@ struct MsmScratchSizes {
     }
 };
 
+// narrow levels' T sums batched into one launch after the last level (MBLS_DEFER_TREES=0: per
+// level on the side stream)
+inline bool defer_narrow_trees() {
+    static const bool v = [] {
+        const char* e = getenv("MBLS_DEFER_TREES");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 // batch members on two pipeline streams (default; MBLS_BATCH_PIPE=0 runs them in order on the
 // caller's stream)
 inline bool batch_pipeline() {
@@ -680,6 +710,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     // joined before the window Horner.
     const uint8_t* V = buckets;
     size_t lvoff = 0;
+    TreeJobs jobs;
+    int njobs = 0;
     for (int l = 0; l < P.levels; ++l) {
         const uint32_t m_in = P.level_m[l];
         const uint32_t seg = P.seg(l);
@@ -697,7 +729,17 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             hipLaunchKernelGGL((k_reduce_level<F, MODE_WAVE>), dim3((chains * 64 + 255) / 256), dim3(256), 0, st, V,
                                m_in, seg, P.Wg, 0, T, R);
         }
-        // sum of this level's T per window: tree stages until one point per window
+        // sum of this level's T per window: narrow levels are batched after the last level;
+        // wide ones run tree stages on the side stream, overlapped with the next levels
+        if (m_out <= TREE_BLOCK_POINTS && defer_narrow_trees()) {
+            jobs.V[njobs] = T;
+            jobs.m[njobs] = m_out;
+            jobs.out[njobs] = sums + (size_t)l * P.Wg * JAC;
+            ++njobs;
+            V = R;
+            lvoff += (size_t)m_out * P.Wg;
+            continue;
+        }
         MBLS_TRY(hipEventRecord(ctx.events[l], st));
         MBLS_TRY(hipStreamWaitEvent(side, ctx.events[l], 0));
         const uint8_t* src = T;
@@ -716,6 +758,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         V = R;
         lvoff += (size_t)m_out * P.Wg;
     }
+    if (njobs) hipLaunchKernelGGL(k_tree_sum_jobs<F>, dim3(njobs * P.Wg), dim3(256), 0, st, jobs, P.Wg);
     MBLS_TRY(hipEventRecord(ctx.events[P.levels], side));
     MBLS_TRY(hipStreamWaitEvent(st, ctx.events[P.levels], 0));
     hipLaunchKernelGGL((k_window_horner<F, MODE_WAVE>), dim3(P.Wg), dim3(64), 0, st, sums, P.levels, P.Wg,
