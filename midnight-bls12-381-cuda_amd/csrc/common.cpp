@@ -78,8 +78,12 @@ StreamCtx& stream_ctx(hipStream_t s) {
     return *it->second;
 }
 
-eIcicleError StreamCtx::ensure_side(size_t nevents) {
-    if (!side) MBLS_TRY(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+eIcicleError StreamCtx::ensure_side(size_t nevents, size_t nsides) {
+    while (sides.size() < nsides) {
+        hipStream_t s;
+        MBLS_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        sides.push_back(s);
+    }
     while (events.size() < nevents) {
         hipEvent_t e;
         MBLS_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));

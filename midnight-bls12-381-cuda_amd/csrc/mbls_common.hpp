@@ -53,7 +53,7 @@ struct StreamCtx {
     // side stream for latency-bound work that overlaps the main chain (MSM tree sums);
     // forked from / joined back into the caller's stream with events, so callers see one
     // stream-ordered operation
-    hipStream_t side = nullptr;
+    std::vector<hipStream_t> sides;
     std::vector<hipEvent_t> events;
     // batch pipeline: two private streams (each with its own StreamCtx / arena) that run
     // alternate batch members, so one member's latency-bound tail overlaps the next member's
@@ -61,7 +61,7 @@ struct StreamCtx {
     hipStream_t pipe[2] = {nullptr, nullptr};
     hipEvent_t pipe_ev[3] = {nullptr, nullptr, nullptr};
     explicit StreamCtx(hipStream_t s) : arena(s) {}
-    eIcicleError ensure_side(size_t nevents);
+    eIcicleError ensure_side(size_t nevents, size_t nsides = 1);
     eIcicleError ensure_pipe();
 };
 StreamCtx& stream_ctx(hipStream_t s);

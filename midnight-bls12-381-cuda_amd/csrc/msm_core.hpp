@@ -312,13 +312,13 @@ __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict_
 // 16 rows sums `per_row` consecutive points, then a 4-level LDS tree.  out[w*nblk + b].
 static constexpr int TREE_PER_ROW = 8;
 template <class F>
-MBLS_DEV void tree_sum_block(const uint8_t* __restrict__ V, uint32_t m, uint32_t w, uint32_t blk,
+MBLS_DEV void tree_sum_block(const uint8_t* __restrict__ V, uint32_t m, uint32_t w, uint32_t blk, uint32_t per_row,
                              uint8_t* __restrict__ out, uint32_t out_idx) {
     __shared__ __attribute__((aligned(16))) uint8_t sh[16 * 3 * sizeof(F)];
     const uint32_t r = threadIdx.x >> 4;  // row in block
     RJac<F> acc = RJac<F>::inf();
-    const uint32_t k0 = (blk * 16 + r) * TREE_PER_ROW;
-    for (uint32_t k = k0; k < min(k0 + TREE_PER_ROW, m); ++k) acc = jac_add(acc, rload_jac<F>(V, (size_t)w * m + k));
+    const uint32_t k0 = (blk * 16 + r) * per_row;
+    for (uint32_t k = k0; k < min(k0 + per_row, m); ++k) acc = jac_add(acc, rload_jac<F>(V, (size_t)w * m + k));
     rstore_jac<F>(sh, r, acc);
     __syncthreads();
     for (uint32_t s = 8; s > 0; s >>= 1) {
@@ -334,13 +334,14 @@ MBLS_DEV void tree_sum_block(const uint8_t* __restrict__ V, uint32_t m, uint32_t
 template <class F>
 __global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V, uint32_t m, uint32_t nblk,
                                                   uint8_t* __restrict__ out) {
-    tree_sum_block<F>(V, m, blockIdx.x / nblk, blockIdx.x % nblk, out, blockIdx.x);
+    tree_sum_block<F>(V, m, blockIdx.x / nblk, blockIdx.x % nblk, TREE_PER_ROW, out, blockIdx.x);
 }
 
-// the narrow levels' T sums (<= one tree block per window each), all in one launch after the
-// last level: block (job, window).  Forked per level they serialised on the side stream
-// (~90 us each) behind the main chain.
-static constexpr uint32_t TREE_BLOCK_POINTS = 16 * TREE_PER_ROW;
+// the narrowest levels' T sums (<= 2 points per row), all in one launch after the last level:
+// block (job, window), ceil(m / 16) points per row then the 4-level LDS tree.  Forked per level
+// they queued behind the wide levels' trees on the side streams (~90 us each).
+static constexpr uint32_t TREE_DEFER_POINTS = 32;
+static constexpr int TREE_SIDES = 3;  // side streams for the wide levels' trees (round robin)
 struct TreeJobs {
     const uint8_t* V[MAX_LEVELS];
     uint8_t* out[MAX_LEVELS];
@@ -349,7 +350,7 @@ struct TreeJobs {
 template <class F>
 __global__ __launch_bounds__(256) void k_tree_sum_jobs(TreeJobs jobs, int Wg) {
     const uint32_t j = blockIdx.x / Wg, w = blockIdx.x % Wg;
-    tree_sum_block<F>(jobs.V[j], jobs.m[j], w, 0, jobs.out[j], w);
+    tree_sum_block<F>(jobs.V[j], jobs.m[j], w, 0, (jobs.m[j] + 15) / 16, jobs.out[j], w);
 }
 
 // G_w = sumT[0] + seg_0*(sumT[1] + seg_1*(sumT[2] + ...)): sums[l * Wg + w]; one chain per window
@@ -535,7 +536,7 @@ struct MsmScratchSizes {
     size_t dsrc, keys, vals, ranks, sorted, words, tmp, owner, first, partials, buckets, levelT, levelR, sums, windows, treetmp, phi;
     size_t total() const {
         return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + first + partials + buckets + levelT + levelR + sums + windows +
-               2 * treetmp + phi;
+               2 * TREE_SIDES * treetmp + phi;
     }
 };
 
@@ -635,17 +636,18 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint8_t* levelR = (uint8_t*)arena.take(z.levelR);
     uint8_t* sums = (uint8_t*)arena.take(z.sums);
     uint8_t* windows = (uint8_t*)arena.take(z.windows);
-    uint8_t* tree_a = (uint8_t*)arena.take(z.treetmp);
-    uint8_t* tree_b = (uint8_t*)arena.take(z.treetmp);
+    uint8_t* tree_tmp[TREE_SIDES][2];
+    for (int k = 0; k < TREE_SIDES; ++k)
+        for (int h = 0; h < 2; ++h) tree_tmp[k][h] = (uint8_t*)arena.take(z.treetmp);
     uint8_t* phi = P.split > 1 ? (uint8_t*)arena.take(z.phi) : nullptr;
-    if (!tree_b || (P.split > 1 && !phi)) return MBLS_ALLOCATION_FAILED;
+    if (!tree_tmp[TREE_SIDES - 1][1] || (P.split > 1 && !phi)) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
     // side stream: the phi(P) table and the heavy-bucket passes overlap the main chain; the
     // per-level tree sums of the reduction run there too.  Events [levels+1 ..) fork / join.
-    if ((er = ctx.ensure_side((size_t)P.levels + 5)) != MBLS_SUCCESS) return er;
-    hipStream_t side = use_side ? ctx.side : st;
+    if ((er = ctx.ensure_side((size_t)P.levels + 5 + TREE_SIDES, TREE_SIDES)) != MBLS_SUCCESS) return er;
+    hipStream_t side = use_side ? ctx.sides[0] : st;
     hipEvent_t* ev = ctx.events.data() + P.levels + 1;
     if (P.split > 1) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
         MBLS_TRY(hipEventRecord(ev[0], st));
@@ -711,7 +713,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     const uint8_t* V = buckets;
     size_t lvoff = 0;
     TreeJobs jobs;
-    int njobs = 0;
+    int njobs = 0, ntree = 0;
+    bool used[TREE_SIDES] = {};
     for (int l = 0; l < P.levels; ++l) {
         const uint32_t m_in = P.level_m[l];
         const uint32_t seg = P.seg(l);
@@ -731,7 +734,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         }
         // sum of this level's T per window: narrow levels are batched after the last level;
         // wide ones run tree stages on the side stream, overlapped with the next levels
-        if (m_out <= TREE_BLOCK_POINTS && defer_narrow_trees()) {
+        if (m_out <= TREE_DEFER_POINTS && defer_narrow_trees()) {
             jobs.V[njobs] = T;
             jobs.m[njobs] = m_out;
             jobs.out[njobs] = sums + (size_t)l * P.Wg * JAC;
@@ -740,16 +743,19 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             lvoff += (size_t)m_out * P.Wg;
             continue;
         }
+        const int sk = ntree++ % TREE_SIDES;
+        hipStream_t ts = use_side ? ctx.sides[sk] : st;
+        used[sk] = true;
         MBLS_TRY(hipEventRecord(ctx.events[l], st));
-        MBLS_TRY(hipStreamWaitEvent(side, ctx.events[l], 0));
+        MBLS_TRY(hipStreamWaitEvent(ts, ctx.events[l], 0));
         const uint8_t* src = T;
         uint32_t m = m_out;
-        uint8_t* pp[2] = {tree_a, tree_b};
+        uint8_t** pp = tree_tmp[sk];
         int flip = 0;
         while (true) {
             const uint32_t nblk = tree_blocks(m);
             uint8_t* dst = (nblk == 1) ? sums + (size_t)l * P.Wg * JAC : pp[flip];
-            hipLaunchKernelGGL(k_tree_sum<F>, dim3(P.Wg * nblk), dim3(256), 0, side, src, m, nblk, dst);
+            hipLaunchKernelGGL(k_tree_sum<F>, dim3(P.Wg * nblk), dim3(256), 0, ts, src, m, nblk, dst);
             if (nblk == 1) break;
             src = dst;
             m = nblk;
@@ -759,8 +765,13 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         lvoff += (size_t)m_out * P.Wg;
     }
     if (njobs) hipLaunchKernelGGL(k_tree_sum_jobs<F>, dim3(njobs * P.Wg), dim3(256), 0, st, jobs, P.Wg);
-    MBLS_TRY(hipEventRecord(ctx.events[P.levels], side));
-    MBLS_TRY(hipStreamWaitEvent(st, ctx.events[P.levels], 0));
+    // join the side streams (the first also carried the table / heavy-bucket work)
+    for (int k = 0; k < TREE_SIDES && use_side; ++k) {
+        if (!used[k] && k > 0) continue;
+        hipEvent_t je = k == 0 ? ctx.events[P.levels] : ev[3 + k];
+        MBLS_TRY(hipEventRecord(je, ctx.sides[k]));
+        MBLS_TRY(hipStreamWaitEvent(st, je, 0));
+    }
     hipLaunchKernelGGL((k_window_horner<F, MODE_WAVE>), dim3(P.Wg), dim3(64), 0, st, sums, P.levels, P.Wg,
                        P.seg_logs_packed(), windows);
     {
