@@ -568,31 +568,42 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_tiled(const uint32_t* __r
 // digit sources per scalar: GLV 2 x 16 B, psi 4 x 16 B, plain standard scalars 32 B
 size_t digits_src_bytes(uint32_t n, int split) { return (size_t)n * (split == 4 ? 64 : 32); }
 
+// the tiled digit kernels' sources: split halves / quarters (sign-magnitude uint4s) or
+// standard-form scalars; nidx = digit-source entries
+static eIcicleError digit_sources(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint8_t* dsrc,
+                                  hipStream_t st, const uint32_t*& src, uint32_t& nidx) {
+    dim3 g((n + 255) / 256);
+    if (P.split == 2) {
+        if (mont)
+            hipLaunchKernelGGL(k_glv_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+        else
+            hipLaunchKernelGGL(k_glv_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+        src = (const uint32_t*)dsrc;
+        nidx = 2 * n;
+    } else if (P.split == 4) {
+        if (mont)
+            hipLaunchKernelGGL(k_psi_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+        else
+            hipLaunchKernelGGL(k_psi_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+        src = (const uint32_t*)dsrc;
+        nidx = 4 * n;
+    } else {
+        if (mont) hipLaunchKernelGGL(k_scalars_std, g, dim3(256), 0, st, scalars, n, dsrc);
+        src = (const uint32_t*)(mont ? dsrc : scalars);
+        nidx = n;
+    }
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
+}
+
 eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* keys,
                            uint32_t* vals, uint32_t* ranks, uint32_t* counts, uint8_t* dsrc, hipStream_t st) {
     dim3 g((n + 255) / 256);
     if (P.B <= DT_MAX_B) {
         const uint32_t* src;
         uint32_t nidx;
-        if (P.split == 2) {
-            if (mont)
-                hipLaunchKernelGGL(k_glv_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
-            else
-                hipLaunchKernelGGL(k_glv_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
-            src = (const uint32_t*)dsrc;
-            nidx = 2 * n;
-        } else if (P.split == 4) {
-            if (mont)
-                hipLaunchKernelGGL(k_psi_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
-            else
-                hipLaunchKernelGGL(k_psi_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
-            src = (const uint32_t*)dsrc;
-            nidx = 4 * n;
-        } else {
-            if (mont) hipLaunchKernelGGL(k_scalars_std, g, dim3(256), 0, st, scalars, n, dsrc);
-            src = (const uint32_t*)(mont ? dsrc : scalars);
-            nidx = n;
-        }
+        eIcicleError er = digit_sources(scalars, mont, n, P, dsrc, st, src, nidx);
+        if (er != MBLS_SUCCESS) return er;
         const uint32_t tiles = (nidx + DT_TILE - 1) / DT_TILE;
         dim3 gt(tiles * (uint32_t)P.W);
         if (P.split > 1)  // GLV / psi sources share the sign-magnitude uint4 format
@@ -700,6 +711,250 @@ eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint3
     hipLaunchKernelGGL(k_scan_local, dim3(nb), dim3(256), 0, st, in, out, tmp, m);
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(256), 0, st, tmp, nb, tmp + nb);
     hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(256), 0, st, out, tmp, m, tmp + nb);
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
+}
+
+// ------------------------------------------------------------------------------------
+// 2b. partitioned counting sort (c <= 16), replacing keys / vals / ranks + the random scatter.
+//   pass A (k_digits_part): workgroup (tile, window) = one SEGMENT buckets its tile's digits
+//     into NP <= 256 coarse PARTS (the top bits of bucket - 1) in LDS and writes them
+//     part-contiguously into its own DT_TILE-entry slice of `ent`, each entry carrying the FB
+//     fine bits; per-part totals go to part_tot with NP coalesced atomics per workgroup.
+//   pass B (k_part_sort): workgroup (window group, part) gathers that part from every segment
+//     of its windows, counts its 2^FB fine buckets in LDS, writes their counts / offsets and
+//     places the entries into the part's span of `sorted`.
+//   Every global write lands in a region one workgroup owns (its slice of ent, its part's span
+//   of sorted), so L2 assembles whole lines instead of 4-byte random writes reaching HBM.
+//   Entry: packed (val | fine << (32 - FB)) when val < 2^(32 - FB), else uint2 {fine, val}.
+// ------------------------------------------------------------------------------------
+static int part_fine_bits(uint32_t B) {
+    const int lb = 31 - __builtin_clz(B);
+    return lb > 8 ? lb - 8 : 0;
+}
+
+bool partition_sort(const MsmPlan& P) {
+    static const bool on = [] {
+        const char* e = getenv("MBLS_PART_SORT");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on && P.B <= DT_MAX_B;
+}
+
+PartSortSizes part_sort_sizes(const MsmPlan& P) {
+    PartSortSizes s;
+    const size_t nidx = P.split > 1 ? P.pts : P.pts / P.F;
+    s.FB = part_fine_bits(P.B);
+    s.NP = P.B >> s.FB;
+    s.tiles = (uint32_t)((nidx + DT_TILE - 1) / DT_TILE);
+    s.segments = s.tiles * (uint32_t)P.W;
+    s.pack = (uint64_t)P.pts <= (1ull << (31 - s.FB));
+    s.ent = (size_t)s.segments * DT_TILE * (s.pack ? 4 : 8);
+    s.segtab = (size_t)s.segments * s.NP * 4;
+    s.parts = ((size_t)P.Wg * s.NP + 1) * 4;
+    return s;
+}
+
+template <bool SPLIT, bool PACK>
+__global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __restrict__ src, uint32_t nidx, int c,
+                                                            int Wg, uint32_t F, uint32_t B, int FB, uint32_t NP,
+                                                            uint32_t* __restrict__ ent, uint32_t* __restrict__ seg_off,
+                                                            uint32_t* __restrict__ seg_cnt,
+                                                            uint32_t* __restrict__ part_tot) {
+    __shared__ uint32_t hist[256];
+    constexpr int NW = SPLIT ? 4 : 8;
+    const uint32_t tiles = (nidx + DT_TILE - 1) / DT_TILE;
+    const uint32_t seg = blockIdx.x;  // w * tiles + tile
+    const uint32_t tile = seg % tiles;
+    const int w = (int)(seg / tiles);
+    const uint32_t wl = SPLIT ? (uint32_t)w : (uint32_t)(w % Wg), f = SPLIT ? 0u : (uint32_t)(w / Wg);
+    if (threadIdx.x < 256) hist[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t dig[DT_PER], lr[DT_PER];
+#pragma unroll
+    for (int k = 0; k < DT_PER; ++k) {
+        const uint32_t idx = tile * DT_TILE + k * DT_THREADS + threadIdx.x;
+        dig[k] = 0;
+        lr[k] = 0;
+        if (idx < nidx) {
+            uint32_t x[NW];
+            const uint4* p = reinterpret_cast<const uint4*>(src) + (size_t)idx * (NW / 4);
+#pragma unroll
+            for (int q = 0; q < NW / 4; ++q) {
+                const uint4 u = p[q];
+                x[4 * q] = u.x;
+                x[4 * q + 1] = u.y;
+                x[4 * q + 2] = u.z;
+                x[4 * q + 3] = u.w;
+            }
+            uint32_t negh = 0;
+            if (SPLIT) {
+                negh = x[3] >> 31;
+                x[3] &= 0x7fffffffu;
+            }
+            const uint32_t d = digit_at<NW>(x, w, c, B) ^ (negh << 31);
+            dig[k] = d;
+            if (d & 0x7fffffffu) lr[k] = atomicAdd(&hist[((d & 0x7fffffffu) - 1) >> FB], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // wave 0: exclusive scan of the NP part sizes, 4 per lane
+        const uint32_t l = threadIdx.x;
+        uint32_t h[4], s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            h[k] = 4 * l + k < NP ? hist[4 * l + k] : 0u;
+            s += h[k];
+        }
+        uint32_t run = wave_incl_scan(s) - s;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t j = 4 * l + k;
+            if (j < NP) {
+                hist[j] = run;
+                seg_off[seg * NP + j] = run;
+                seg_cnt[seg * NP + j] = h[k];
+                if (h[k]) atomicAdd(&part_tot[wl * NP + j], h[k]);
+            }
+            run += h[k];
+        }
+    }
+    __syncthreads();
+    const uint32_t fmask = (1u << FB) - 1;
+#pragma unroll
+    for (int k = 0; k < DT_PER; ++k) {
+        const uint32_t idx = tile * DT_TILE + k * DT_THREADS + threadIdx.x;
+        const uint32_t v = dig[k] & 0x7fffffffu, sign = dig[k] >> 31;
+        if (idx >= nidx || v == 0) continue;
+        const uint32_t part = (v - 1) >> FB, fine = (v - 1) & fmask;
+        const uint32_t val = ((SPLIT ? idx : idx * F + f) << 1) | sign;
+        const size_t o = (size_t)seg * DT_TILE + hist[part] + lr[k];
+        if (PACK)
+            ent[o] = FB ? (val | (fine << (32 - FB))) : val;
+        else
+            reinterpret_cast<uint2*>(ent)[o] = make_uint2(fine, val);
+    }
+}
+
+template <bool PACK>
+__device__ __forceinline__ void part_entry(const uint32_t* __restrict__ ent, size_t o, int FB, uint32_t& fine,
+                                           uint32_t& val) {
+    if (PACK) {
+        const uint32_t e = ent[o];
+        fine = FB ? e >> (32 - FB) : 0u;
+        val = FB ? e & ((1u << (32 - FB)) - 1) : e;
+    } else {
+        const uint2 e = reinterpret_cast<const uint2*>(ent)[o];
+        fine = e.x;
+        val = e.y;
+    }
+}
+
+// teams of PS_TEAM lanes walk the segments of the workgroup's windows (64 B contiguous per
+// team and load when packed)
+static constexpr uint32_t PS_TEAM = 16;
+
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ ent, const uint32_t* __restrict__ seg_off,
+                                                   const uint32_t* __restrict__ seg_cnt,
+                                                   const uint32_t* __restrict__ part_base, uint32_t tiles, int W,
+                                                   int Wg, uint32_t B, int FB, uint32_t NP,
+                                                   uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets,
+                                                   uint32_t* __restrict__ sorted) {
+    __shared__ uint32_t cnt[128], pre[128];
+    const uint32_t FBN = 1u << FB;
+    const uint32_t wl = blockIdx.x / NP, part = blockIdx.x % NP;
+    // windows of group wl: wl, wl + Wg, ... < W (precompute factor F > 1), `tiles` segments each
+    const uint32_t S = ((uint32_t)(W - 1 - (int)wl) / (uint32_t)Wg + 1) * tiles;
+    const uint32_t team = threadIdx.x / PS_TEAM, tl = threadIdx.x % PS_TEAM, nteams = 256 / PS_TEAM;
+    if (threadIdx.x < FBN) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t s = team; s < S; s += nteams) {
+        const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
+        const uint32_t k = seg_cnt[seg * NP + part];
+        const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
+        for (uint32_t i = tl; i < k; i += PS_TEAM) {
+            uint32_t fine, val;
+            part_entry<PACK>(ent, o + i, FB, fine, val);
+            atomicAdd(&cnt[fine], 1u);
+        }
+    }
+    __syncthreads();
+    const uint32_t base = part_base[wl * NP + part];
+    if (threadIdx.x < 64) {  // wave 0: exclusive scan of the FBN <= 128 fine counts, 2 per lane
+        const uint32_t l = threadIdx.x;
+        const uint32_t h0 = 2 * l < FBN ? cnt[2 * l] : 0u, h1 = 2 * l + 1 < FBN ? cnt[2 * l + 1] : 0u;
+        const uint32_t run = wave_incl_scan(h0 + h1) - (h0 + h1);
+        const size_t key = (size_t)wl * B + part * FBN + 2 * l;
+        if (2 * l < FBN) {
+            pre[2 * l] = run;
+            counts[key] = h0;
+            offsets[key] = base + run;
+        }
+        if (2 * l + 1 < FBN) {
+            pre[2 * l + 1] = run + h0;
+            counts[key + 1] = h1;
+            offsets[key + 1] = base + run + h0;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 64) offsets[(size_t)Wg * B] = part_base[(size_t)Wg * NP];
+    __syncthreads();
+    if (threadIdx.x < FBN) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t s = team; s < S; s += nteams) {
+        const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
+        const uint32_t k = seg_cnt[seg * NP + part];
+        const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
+        for (uint32_t i = tl; i < k; i += PS_TEAM) {
+            uint32_t fine, val;
+            part_entry<PACK>(ent, o + i, FB, fine, val);
+            sorted[base + pre[fine] + atomicAdd(&cnt[fine], 1u)] = val;
+        }
+    }
+}
+
+eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* ent,
+                                uint32_t* seg_off, uint32_t* seg_cnt, uint32_t* part_tot, uint8_t* dsrc,
+                                hipStream_t st) {
+    if (P.B > DT_MAX_B) return MBLS_INVALID_ARGUMENT;
+    const PartSortSizes z = part_sort_sizes(P);
+    const uint32_t* src;
+    uint32_t nidx;
+    eIcicleError er = digit_sources(scalars, mont, n, P, dsrc, st, src, nidx);
+    if (er != MBLS_SUCCESS) return er;
+    MBLS_TRY(hipMemsetAsync(part_tot, 0, (size_t)P.Wg * z.NP * 4, st));
+    dim3 g(z.segments), b(DT_THREADS);
+    const uint32_t F = (uint32_t)P.F;
+#define MBLS_DP(S_, P_)                                                                                           \
+    hipLaunchKernelGGL((k_digits_part<S_, P_>), g, b, 0, st, src, nidx, P.c, P.Wg, F, P.B, z.FB, z.NP, ent, seg_off, \
+                       seg_cnt, part_tot)
+    if (P.split > 1) {
+        if (z.pack)
+            MBLS_DP(true, true);
+        else
+            MBLS_DP(true, false);
+    } else if (z.pack)
+        MBLS_DP(false, true);
+    else
+        MBLS_DP(false, false);
+#undef MBLS_DP
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
+}
+
+eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint32_t* seg_off, const uint32_t* seg_cnt,
+                              const uint32_t* part_tot, uint32_t* part_base, uint32_t* tmp, uint32_t* counts,
+                              uint32_t* offsets, uint32_t* sorted, hipStream_t st) {
+    const PartSortSizes z = part_sort_sizes(P);
+    eIcicleError er = scan_exclusive(part_tot, part_base, (uint32_t)P.Wg * z.NP, tmp, st);
+    if (er != MBLS_SUCCESS) return er;
+    dim3 g((uint32_t)P.Wg * z.NP), b(256);
+    if (z.pack)
+        hipLaunchKernelGGL(k_part_sort<true>, g, b, 0, st, ent, seg_off, seg_cnt, part_base, z.tiles, P.W, P.Wg, P.B,
+                           z.FB, z.NP, counts, offsets, sorted);
+    else
+        hipLaunchKernelGGL(k_part_sort<false>, g, b, 0, st, ent, seg_off, seg_cnt, part_base, z.tiles, P.W, P.Wg, P.B,
+                           z.FB, z.NP, counts, offsets, sorted);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }

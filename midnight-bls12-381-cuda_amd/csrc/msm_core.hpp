@@ -86,6 +86,23 @@ eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hi
 eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
 size_t scan_tmp_words(uint32_t m);
 
+// partitioned counting sort (msm_common.hip 2b): pass A digits -> per-segment coarse parts,
+// pass B per-part LDS counting sort.  Replaces keys / vals / ranks + k_scatter for c <= 16.
+struct PartSortSizes {
+    uint32_t NP = 0, tiles = 0, segments = 0;
+    int FB = 0;
+    bool pack = false;
+    size_t ent = 0, segtab = 0, parts = 0;  // bytes
+};
+bool partition_sort(const MsmPlan& P);
+PartSortSizes part_sort_sizes(const MsmPlan& P);
+eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* ent,
+                                uint32_t* seg_off, uint32_t* seg_cnt, uint32_t* part_tot, uint8_t* dsrc,
+                                hipStream_t st);
+eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint32_t* seg_off, const uint32_t* seg_cnt,
+                              const uint32_t* part_tot, uint32_t* part_base, uint32_t* tmp, uint32_t* counts,
+                              uint32_t* offsets, uint32_t* sorted, hipStream_t st);
+
 // ------------------------------------------------------------------------------------
 // 4. accumulation: thread t sums the 16 contributions at sorted positions [16t, 16t + 16),
 //    one partial per bucket segment it touches (see k_chunk_counts): no idle lanes on the
@@ -534,9 +551,10 @@ struct GroupTraits<Fq2> {
 
 struct MsmScratchSizes {
     size_t dsrc, keys, vals, ranks, sorted, words, tmp, owner, first, partials, buckets, levelT, levelR, sums, windows, treetmp, phi;
+    size_t ent, segtab, parts;  // partitioned sort (keys / vals / ranks are 0 then)
     size_t total() const {
         return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + first + partials + buckets + levelT + levelR + sums + windows +
-               2 * TREE_SIDES * treetmp + phi;
+               2 * TREE_SIDES * treetmp + phi + ent + 2 * segtab + 2 * parts;
     }
 };
 
@@ -574,9 +592,18 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     MsmScratchSizes z;
     z.phi = P.split > 1 ? align_up(P.pts / P.split * (P.split - 1) * aff) : 0;
     const size_t NC = P.contributions;
-    z.keys = align_up(NC * 4);
-    z.vals = align_up(NC * 4);
-    z.ranks = align_up(NC * 4);
+    if (partition_sort(P)) {
+        const PartSortSizes s = part_sort_sizes(P);
+        z.keys = z.vals = z.ranks = 0;
+        z.ent = align_up(s.ent);
+        z.segtab = align_up(s.segtab);
+        z.parts = align_up(s.parts);
+    } else {
+        z.keys = align_up(NC * 4);
+        z.vals = align_up(NC * 4);
+        z.ranks = align_up(NC * 4);
+        z.ent = z.segtab = z.parts = 0;
+    }
     z.dsrc = align_up(digits_src_bytes((uint32_t)(P.split > 1 ? P.pts / P.split : P.pts / P.F), P.split));
     z.sorted = align_up(NC * 4);
     z.words = align_up(((size_t)P.TB + 1) * 4);
@@ -640,7 +667,13 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     for (int k = 0; k < TREE_SIDES; ++k)
         for (int h = 0; h < 2; ++h) tree_tmp[k][h] = (uint8_t*)arena.take(z.treetmp);
     uint8_t* phi = P.split > 1 ? (uint8_t*)arena.take(z.phi) : nullptr;
-    if (!tree_tmp[TREE_SIDES - 1][1] || (P.split > 1 && !phi)) return MBLS_ALLOCATION_FAILED;
+    const bool psort = partition_sort(P);
+    uint32_t* ent = (uint32_t*)arena.take(z.ent);
+    uint32_t* seg_off = (uint32_t*)arena.take(z.segtab);
+    uint32_t* seg_cnt = (uint32_t*)arena.take(z.segtab);
+    uint32_t* part_tot = (uint32_t*)arena.take(z.parts);
+    uint32_t* part_base = (uint32_t*)arena.take(z.parts);
+    if (!tree_tmp[TREE_SIDES - 1][1] || (P.split > 1 && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
@@ -658,16 +691,25 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     }
     {
         ProfScope ps("msm.digits", st);
-        MBLS_TRY(hipMemsetAsync(counts, 0, (size_t)TB * 4, st));
-        er = launch_digits(scalars, scalars_mont, n, P, keys, vals, ranks, counts, dsrc, st);
+        if (psort) {
+            er = launch_digits_part(scalars, scalars_mont, n, P, ent, seg_off, seg_cnt, part_tot, dsrc, st);
+        } else {
+            MBLS_TRY(hipMemsetAsync(counts, 0, (size_t)TB * 4, st));
+            er = launch_digits(scalars, scalars_mont, n, P, keys, vals, ranks, counts, dsrc, st);
+        }
         if (er != MBLS_SUCCESS) return er;
     }
     {
         ProfScope ps("msm.sort", st);
-        if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) return er;
+        if (psort) {  // writes counts, offsets (incl. offsets[TB]) and sorted
+            er = launch_part_sort(P, ent, seg_off, seg_cnt, part_tot, part_base, tmp, counts, offsets, sorted, st);
+            if (er != MBLS_SUCCESS) return er;
+        } else if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) {
+            return er;
+        }
         if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, st)) != MBLS_SUCCESS) return er;
         if ((er = scan_exclusive(nchunks, chunk_off, TB, tmp, st)) != MBLS_SUCCESS) return er;
-        if ((er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
+        if (!psort && (er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
         if ((er = launch_chunk_owner(chunk_off, offsets, TB, owner, first, st)) != MBLS_SUCCESS) return er;
     }
     {

@@ -6,5 +6,5 @@ i=0
 for S in "$@"; do
   i=$((i+1))
   env $S timeout -k 10 200 python bench.py --no-cpu --no-mix --steps 10 > gpurun_out/sweep/$i.json 2> gpurun_out/sweep/$i.err || exit $?
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); s=d['msm_stage_ms']; print(sys.argv[2], '|', d['value'], '| red', s['msm.reduce'], 'fin', s['msm.final'], 'bs', s['msm.bucket_sum'])" gpurun_out/sweep/$i.json "$S"
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); s=d['msm_stage_ms']; print(sys.argv[2], '|', d['value'], '| dig', s['msm.digits'], 'sort', s['msm.sort'], 'acc', s['msm.accumulate'], 'red', s['msm.reduce'], 'fin', s['msm.final'], 'bs', s['msm.bucket_sum'])" gpurun_out/sweep/$i.json "$S"
 done
