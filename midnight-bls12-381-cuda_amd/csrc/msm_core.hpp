@@ -12,6 +12,8 @@
 //   2. scans          bucket offsets; buckets are split in chunks of <= CHUNK points so one
 //                     heavy bucket (e.g. all-equal scalars) cannot serialise a thread.
 //   3. k_scatter      counting-sort scatter (keys < TB: no radix sort needed).
+//      c <= 16 (default): steps 1-3 are the partitioned counting sort instead
+//                     (k_digits_part + k_part_sort, msm_common.hip 2b).
 //   4. k_accumulate   one thread per chunk: sum of +-P_i by mixed additions -> partial.
 //   5. k_bucket_sum   one thread per bucket: sum of its chunk partials.
 //   6. bucket reduction sum_d d*B_d per window as a recursive running-sum: level l splits
@@ -35,6 +37,11 @@
 #include "mbls_curve.hpp"
 #include "mbls_rowfield.hpp"
 #include "mbls_wavepoint.hpp"
+#include "mbls_xyzz.hpp"
+
+#ifndef MBLS_XYZZ
+#define MBLS_XYZZ 0  // 1: k_accumulate in XYZZ coordinates (measured slower: 3.51 vs 3.15 ms at G1 2^20, register pressure)
+#endif
 
 namespace mbls {
 
@@ -134,6 +141,28 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
     // one point ahead: the next random 96/192-byte fetch overlaps this mixed addition
     uint32_t v = sorted[beg];
     Affine<L> p = fetch(v);
+#if MBLS_XYZZ
+    // XYZZ accumulator (mbls_xyzz.hpp); one flush site converts to the Jacobian partial
+    XYZZ<L> xa = XYZZ<L>::inf();
+    for (uint32_t e = beg;; ++e) {
+        if (e == bend || e == end) {  // bucket boundary or chunk end: flush
+            store_jac<L>(partials, seg, xyzz_to_jac(xa));
+            if (e == end) break;
+            xa = XYZZ<L>::inf();
+            do {
+                ++b;
+            } while (offsets[b + 1] == e);  // skip empty buckets
+            seg = chunk_off[b];
+            bend = offsets[b + 1];
+        }
+        const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
+        const Affine<L> pn = fetch(vn);
+        xa = xyzz_madd(xa, (v & 1) ? aff_neg(p) : p);
+        v = vn;
+        p = pn;
+    }
+    (void)acc;
+#else
     for (uint32_t e = beg; e < end; ++e) {
         if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
             store_jac<L>(partials, seg, acc);
@@ -151,6 +180,7 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
         p = pn;
     }
     store_jac<L>(partials, seg, acc);
+#endif
 }
 
 // ------------------------------------------------------------------------------------
