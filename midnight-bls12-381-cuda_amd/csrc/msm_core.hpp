@@ -40,7 +40,7 @@
 #include "mbls_xyzz.hpp"
 
 #ifndef MBLS_XYZZ
-#define MBLS_XYZZ 0  // 1: k_accumulate in XYZZ coordinates (measured slower: 3.51 vs 3.15 ms at G1 2^20, register pressure)
+#define MBLS_XYZZ 0  // 1: k_accumulate in XYZZ coordinates (measured slower: 3.49 vs 3.15 ms at G1 2^20)
 #endif
 
 namespace mbls {
