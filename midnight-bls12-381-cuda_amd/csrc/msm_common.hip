@@ -852,7 +852,10 @@ __device__ __forceinline__ void part_entry(const uint32_t* __restrict__ ent, siz
 
 // teams of PS_TEAM lanes walk the segments of the workgroup's windows (64 B contiguous per
 // team and load when packed)
-static constexpr uint32_t PS_TEAM = 16;
+#ifndef MBLS_PS_TEAM
+#define MBLS_PS_TEAM 16
+#endif
+static constexpr uint32_t PS_TEAM = MBLS_PS_TEAM;
 
 template <bool PACK>
 __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ ent, const uint32_t* __restrict__ seg_off,
