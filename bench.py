@@ -4,18 +4,23 @@
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 launched by
 torch.distributed.run, one rank per GPU.  Rank 0 prints ONE JSON line.
 
-Step = one G1 MSM over N * 2^msm_log points, sharded contiguously: each rank runs Pippenger
-on its 2^msm_log shard (bases device-resident, scalars Montgomery on device -- the
-production path core/msm.rs:594-682), then the partial Jacobian sums are exchanged with one
-RCCL all_gather over xGMI and EC-added on device (reference has no multi-GPU).
-value = MSMs of 2^msm_log points (per-GPU shard size) completed per second over all GPUs
-(weak scaling).  The Fr NTT 2^ntt_log (forward, natural order, best_fft semantics) is timed
-in its own loop on every rank (replicas) and reported as `ntt_per_sec`.
-Inputs are synthetic: seeded scalars and bases P_i = k_i G generated on the device.
+Headline (`value`, BASELINE config #3): one step = one G1 MSM of 2^msm_log points per rank on
+the PRODUCTION path core/msm.rs:594-682 uses -- scalars in Montgomery form and bases resident
+in HBM, the ICICLE entry (bls12_381_icicle_g1_msm: Montgomery flags honoured, ICICLE (x, y, 1)
+standard-form result left on the device).  At N > 1 every rank runs its 2^msm_log shard of one
+global input stream (mbls_g1_msm_jacobian), the Jacobian partials are exchanged with ONE RCCL
+all_gather over xGMI, added on the device and normalised once (the reference has
+no multi-GPU path).  value = MSMs of 2^msm_log points completed per second over all GPUs
+(weak scaling).  The other BASELINE configs are legs of the same run (see `configs` below):
+#1 vecops (GPU and the CPU path), #2 NTT 2^20 round trip, #4 the 2^24 MSM split over the N
+ranks (strong scaling, digest comparable across N), #5 G2 MSM 2^20 + 4 x NTT 2^22 on two
+streams.  Inputs are synthetic: seeded scalars and bases P_i = k_i G generated on the device.
 """
 import argparse
+import hashlib
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -24,20 +29,34 @@ PKG = os.path.join(ROOT, "midnight-bls12-381-cuda_amd")
 sys.path.insert(0, PKG)
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+MAD_RATE_T = 20.9         # measured v_mad_u64_u32 issue rate, T/s (profiles/r01/microbench.txt)
 MSM_BYTES_PER_POINT = 128  # 32 B scalar + 96 B affine base
+G2_BYTES_PER_POINT = 224   # 32 B scalar + 192 B affine base
 NTT_BYTES_PER_ELEM = 64    # one read + one write of 32 B per transform
-# HBM bytes per launch from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
-# (tools/gpu_pmc.sh on tools/pmc_probe.py's fixed workload; gfx950 FETCH_SIZE x2 correction)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+VEC_BYTES_PER_ELEM = 96    # read a, b; write out
+# v_mad_u64_u32 per G1 mixed addition (madd-2007-bl, lazy Y3): 5 Fq products x 288 + 4 squares x
+# 222 + one two-product lazy sum x 432
+MADS_PER_G1_MADD = 5 * 288 + 4 * 222 + 432
+# per Fr butterfly product (FIPS Fr: 64 product mads + 56 reduction mads, r = 1 mod 2^32)
+MADS_PER_FR_MUL = 120
+PROFILES = os.path.join(ROOT, "profiles")
 
 
-def pmc_traffic(kernel, n_launches_per_unit=1):
-    try:
-        with open(PMC_SUMMARY) as f:
-            k = json.load(f)["kernels"].get(kernel)
-        return None if not k or k.get("hbm_bytes_per_launch") is None else k["hbm_bytes_per_launch"] * n_launches_per_unit
-    except (OSError, ValueError, KeyError):
-        return None
+def pmc_summary():
+    for rnd in ("r02", "r01"):
+        path = os.path.join(PROFILES, rnd, "pmc_summary.json")
+        try:
+            with open(path) as f:
+                return json.load(f), os.path.relpath(path, ROOT)
+        except (OSError, ValueError):
+            continue
+    return {}, None
+
+
+def pmc_traffic(kernel):
+    d, _ = pmc_summary()
+    k = d.get("kernels", {}).get(kernel)
+    return None if not k or k.get("hbm_bytes_per_launch") is None else k["hbm_bytes_per_launch"]
 
 
 def parse():
@@ -47,12 +66,21 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--msm-log", type=int, default=20)
     ap.add_argument("--ntt-log", type=int, default=22)
+    ap.add_argument("--msm-total-log", type=int, default=24,
+                    help="config #4: one MSM of 2^k points split over the ranks (0: skip)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0, help="bound on the CPU MSM leg's repeats")
     ap.add_argument("--no-mix", action="store_true", help="skip the G2 MSM + batched NTT overlap leg (config #5)")
     ap.add_argument("--mix-batch", type=int, default=4, help="NTT polynomials in the config #5 batch")
     ap.add_argument("--msm-batch", type=int, default=8, help="members of the batched-MSM leg (0: skip)")
+    ap.add_argument("--headline-only", action="store_true", help="headline MSM + NTT loops only (profiling)")
     return ap.parse_args()
+
+
+def digest(t):
+    import numpy as np
+    return hashlib.sha256(t.detach().cpu().numpy().view(np.uint64).tobytes()).hexdigest()[:16]
 
 
 def main():
@@ -62,7 +90,7 @@ def main():
     import bls12_381_amd as amd
     import sharded_msm
 
-    world =int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -78,25 +106,48 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    # ------------------------------------------------------------------ MSM inputs
+    def max_over_ranks(x):
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(fn, reps, warm=1, sync_all=False):
+        """wall ms per call of fn over `reps` calls (stream-ordered, synchronised at both ends)"""
+        for _ in range(warm):
+            fn()
+        (barrier_sync if sync_all else lambda: torch.cuda.synchronize(dev))()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        (barrier_sync if sync_all else lambda: torch.cuda.synchronize(dev))()
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    # ------------------------------------------------------------------ headline MSM inputs
     n = 1 << args.msm_log
     scalars = torch.zeros((n, 4), dtype=torch.int64, device=dev)
     bases = torch.zeros((n, 12), dtype=torch.int64, device=dev)
-    amd.gen_scalars(scalars, 0x5EED0003 + rank, montgomery=True, stream=stream)
-    amd.gen_bases("g1", bases, 0x5EED0013 + rank, stream=stream)
+    # rank r holds elements [r n, (r + 1) n) of one global stream (N = 1: the test's inputs)
+    amd.gen_scalars(scalars, 0x5EED0003, montgomery=True, stream=stream, start=rank * n)
+    amd.gen_bases("g1", bases, 0x5EED0013, stream=stream, start=rank * n)
+    result = torch.zeros((1, 18), dtype=torch.int64, device=dev)
     partial = torch.zeros((1, 18), dtype=torch.int64, device=dev)
     gathered = torch.zeros((world, 18), dtype=torch.int64, device=dev)
-    total = torch.zeros((1, 18), dtype=torch.int64, device=dev)
     torch.cuda.synchronize(dev)
 
+    def sharded_step(sc, bs, m):
+        """one rank's production-path MSM; N > 1: Jacobian partial -> all_gather -> EC sum ->
+        one (x, y, 1) normalisation (result: ICICLE form on every rank)"""
+        if world == 1:
+            amd.msm("g1", sc, bs, icicle=True, scalars_mont=True, out=result, stream=stream, is_async=True, n=m)
+            return
+        amd.msm("g1", sc, bs, icicle="jacobian", scalars_mont=True, out=partial, stream=stream, is_async=True, n=m)
+        sharded_msm.gather_partials(partial, world, dist, out=gathered)
+        amd.sum_jacobian("g1", gathered, result, stream=stream)
+        amd.jacobian_to_icicle("g1", result, stream=stream)
+
     def msm_step():
-        # bls12_381_g1_msm_cuda semantics (reference icicle_curve_api.cu:679): result is a
-        # Jacobian Montgomery point left on the device, no host round trip
-        amd.msm("g1", scalars, bases, icicle=False, scalars_mont=True, out=partial, stream=stream,
-                is_async=True, n=n)
-        if world > 1:
-            sharded_msm.gather_partials(partial, world, dist, out=gathered)
-            amd.sum_jacobian("g1", gathered, total, stream=stream)
+        sharded_step(scalars, bases, n)
 
     for _ in range(args.warmup):
         msm_step()
@@ -105,101 +156,83 @@ def main():
     for _ in range(args.steps):
         msm_step()
     barrier_sync()
-    dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    msm_time = float(dt_t.item())
+    msm_time = max_over_ranks(time.perf_counter() - t0)
     ms_per_step = msm_time / args.steps * 1e3
     msm_per_sec = world * args.steps / msm_time
+    headline_result = result.clone()
 
-    # batched MSMs (ICICLE batch_size, shared device bases, device results): members pipelined
-    # on two streams so each member's latency-bound reduction overlaps the next accumulation
-    batch_leg = None
-    if args.msm_batch > 1:
-        B = args.msm_batch
-        sb = torch.zeros((B * n, 4), dtype=torch.int64, device=dev)
-        amd.gen_scalars(sb, 0x5EED0033 + rank, montgomery=True, stream=stream)
-        rb = torch.zeros((B, 18), dtype=torch.int64, device=dev)
-
-        def batch_step():
-            amd.msm("g1", sb, bases, icicle=True, scalars_mont=True, batch=B, out=rb, stream=stream,
-                    is_async=True, n=n)
-
-        batch_step()
-        barrier_sync()
-        reps = max(2, args.steps // 4)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            batch_step()
-        barrier_sync()
-        bdt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(bdt, op=dist.ReduceOp.MAX)
-        batch_leg = {"batch": B, "reps": reps, "ms_per_batch": round(float(bdt.item()) / reps * 1e3, 3),
-                     "msm_per_sec": round(world * B * reps / float(bdt.item()), 3),
-                     "note": "ICICLE batch_size (core/msm.rs msm_batch_with_device_bases), members pipelined on two HIP streams"}
-        del sb
-
-    # live per-stage timing (HIP events on this stream) for the roofline
+    # live per-stage timing (HIP events recorded on the MSM's own stream) for the roofline
     amd.profile(True)
-    for _ in range(max(2, args.steps // 2)):
+    for _ in range(max(3, args.steps // 2)):
         msm_step()
     torch.cuda.synchronize(dev)
     msm_prof = amd.profile_read()
     amd.profile(False)
 
-    # ------------------------------------------------------------------ NTT (replicas)
+    extra = {}
+    if not args.headline_only:
+        extra.update(msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_over_ranks, world))
+    # ------------------------------------------------------------------ config #4: 2^total split over ranks
+    cfg4 = None
+    if args.msm_total_log and not args.headline_only:
+        total = 1 << args.msm_total_log
+        lo, hi = sharded_msm.shard_range(total, world, rank)
+        m = hi - lo
+        s4 = torch.zeros((m, 4), dtype=torch.int64, device=dev)
+        b4 = torch.zeros((m, 12), dtype=torch.int64, device=dev)
+        amd.gen_scalars(s4, 0x5EED0004, montgomery=True, stream=stream, start=lo)
+        amd.gen_bases("g1", b4, 0x5EED0013, stream=stream, start=lo)
+        torch.cuda.synchronize(dev)
+        reps = max(2, args.steps // 4)
+        ms4 = max_over_ranks(timed(lambda: sharded_step(s4, b4, m), reps, warm=1, sync_all=True))
+        cfg4 = {"workload": f"G1 MSM 2^{args.msm_total_log} points sharded {world}-way (strong scaling)",
+                "points_per_rank": m, "reps": reps, "ms_per_msm": round(ms4, 3),
+                "msm_per_sec": round(1e3 / ms4, 4),
+                "points_per_sec": round(total / ms4 * 1e3, 1),
+                "result_digest": digest(result),
+                "note": "same result_digest at every N = bit-identical sharded sum; the 1-GPU result is "
+                        "pinned to the oracle by tests/test_gpu_parity.py::test_msm_g1_2_24_single_and_sharded"}
+        del s4, b4
+        torch.cuda.empty_cache()
+
+    # ------------------------------------------------------------------ NTT 2^ntt_log (replicas)
     amd.ntt_init_domain()
     nn = 1 << args.ntt_log
     x = torch.zeros((nn, 4), dtype=torch.int64, device=dev)
     y = torch.zeros_like(x)
-    amd.gen_scalars(x, 0x5EED0025 + rank, montgomery=True, stream=stream)
-    for _ in range(args.warmup):
-        amd.ntt(x, out=y, stream=stream, is_async=True)
-    barrier_sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        amd.ntt(x, out=y, stream=stream, is_async=True)
-    barrier_sync()
-    ndt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(ndt, op=dist.ReduceOp.MAX)
-    ntt_per_sec = world * args.steps / float(ndt.item())
+    amd.gen_scalars(x, 0x5EED0025, montgomery=True, stream=stream)
+    ntt_ms_wall = max_over_ranks(timed(lambda: amd.ntt(x, out=y, stream=stream, is_async=True), args.steps,
+                                       warm=args.warmup, sync_all=True))
+    ntt_per_sec = world * 1e3 / ntt_ms_wall
     amd.profile(True)
-    for _ in range(max(2, args.steps // 2)):
+    for _ in range(max(3, args.steps // 2)):
         amd.ntt(x, out=y, stream=stream, is_async=True)
     torch.cuda.synchronize(dev)
     ntt_prof = amd.profile_read()
     amd.profile(False)
 
-    # NTT 2^20 forward + inverse round trip (BASELINE config #2), device-resident
-    x20 = x[: 1 << 20]
-    y20 = torch.zeros_like(x20)
-    z20 = torch.zeros_like(x20)
-    reps = max(3, args.steps)
-    for _ in range(2):
-        amd.ntt(x20, out=y20, stream=stream, is_async=True)
-        amd.ntt(y20, inverse=True, out=z20, stream=stream, is_async=True)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        amd.ntt(x20, out=y20, stream=stream, is_async=True)
-        amd.ntt(y20, inverse=True, out=z20, stream=stream, is_async=True)
-    torch.cuda.synchronize(dev)
-    ntt20_rt_ms = (time.perf_counter() - t0) / reps * 1e3
-    ntt20_exact = bool(torch.equal(z20, x20))
-    del y20, z20
+    legs = {}
+    if not args.headline_only:
+        # config #2: NTT 2^20 forward + inverse round trip, device-resident
+        x20 = x[: 1 << 20]
+        y20 = torch.zeros_like(x20)
+        z20 = torch.zeros_like(x20)
 
-    # ------------------------------------------------------------------ config #5 mix (replicas)
-    mix = None
-    if not args.no_mix:
-        mix = mix_leg(args, amd, torch, dev, rank)
+        def rt():
+            amd.ntt(x20, out=y20, stream=stream, is_async=True)
+            amd.ntt(y20, inverse=True, out=z20, stream=stream, is_async=True)
+        rt_ms = timed(rt, max(3, args.steps), warm=2)
+        legs["ntt20_roundtrip_ms"] = round(rt_ms, 4)
+        legs["ntt20_roundtrip_exact"] = bool(torch.equal(z20, x20))
+        del y20, z20
+        legs["vecops"] = vecops_leg(amd, torch, dev, stream, timed)
+        if not args.no_mix:
+            legs["mix_g2msm_batched_ntt"] = mix_leg(args, amd, torch, dev, rank, timed)
 
     # ------------------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args, amd, scalars, bases, n)
+    if rank == 0 and world == 1 and not args.no_cpu and not args.headline_only:
+        cpu = cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, x)
 
     if rank == 0:
         def avg(prof, key):
@@ -207,12 +240,16 @@ def main():
             return ms / cnt if cnt else None
 
         acc_ms = avg(msm_prof, "msm.accumulate")
-        msm_total_ms = avg(msm_prof, "msm.total")
         ntt_ms = avg(ntt_prof, "ntt.transform")
         ntt_pass_ms = avg(ntt_prof, "ntt.pass")
         stages = {k: round(v[0] / v[1], 4) for k, v in sorted(msm_prof.items()) if v[1]}
+        # dominant kernel: k_accumulate<G1>; algorithmic bytes = 128 B x points per launch
         msm_ach = MSM_BYTES_PER_POINT * n / (acc_ms * 1e-3) / 1e9 if acc_ms else None
+        contributions = 2 * n * ((128 + 16 - 1) // 16)  # GLV: 2n digit streams x 8 windows (c = 16)
+        mad_t = contributions * MADS_PER_G1_MADD / (acc_ms * 1e-3) / 1e12 if acc_ms else None
         ntt_ach = NTT_BYTES_PER_ELEM * nn / (ntt_ms * 1e-3) / 1e9 if ntt_ms else None
+        ntt_mad_t = (nn // 2) * args.ntt_log * MADS_PER_FR_MUL / (ntt_ms * 1e-3) / 1e12 if ntt_ms else None
+        _, pmc_src = pmc_summary()
         out = {
             "metric": "G1 MSM/sec at 2^20 points + Fr NTT/sec at 2^22 (bit-exact vs BLST)",
             "value": round(msm_per_sec, 3),
@@ -226,9 +263,11 @@ def main():
             "vs_baseline": None,
             "dtype": "u32-limb Montgomery (Fq 381-bit / Fr 255-bit integer)",
             "data": "synthetic: seeded scalars, bases k_i*G generated on device",
-            "config": {"workload": f"G1 MSM 2^{args.msm_log} points per GPU (sharded, RCCL all-gather of "
-                                   f"partial sums) + Fr NTT 2^{args.ntt_log}",
+            "config": {"workload": f"G1 MSM 2^{args.msm_log} points per GPU, production path (ICICLE entry, "
+                                   f"Montgomery scalars + bases in HBM, (x,y,1) result on device); N>1: "
+                                   f"sharded, RCCL all-gather of partial sums",
                        "msm_points_per_gpu": n, "ntt_size": nn, "parallelism": f"msm-shard{world}"},
+            "bit_exact": cpu.get("bit_exact") if cpu else None,
             "ntt_per_sec": round(ntt_per_sec, 3),
             "ntt_ms": round(ntt_ms, 4) if ntt_ms else None,
             "msm_stage_ms": stages,
@@ -237,37 +276,102 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(msm_ach / HBM_PEAK_GBS, 5) if msm_ach else None,
                          "traffic": pmc_traffic("k_accumulate"),
-                         "traffic_source": "profiles/r01/pmc_summary.json (bytes per launch)",
-                         "note": "VALU-bound (v_mad_u64_u32); HBM fraction reported as the contract asks"},
-            "msm_batch": batch_leg,
-            "ntt20_roundtrip_ms": round(ntt20_rt_ms, 4),
-            "ntt20_roundtrip_exact": ntt20_exact,
-            "mix_g2msm_batched_ntt": mix,
+                         "traffic_source": f"{pmc_src} (HBM bytes per launch)" if pmc_src else None,
+                         "note": "VALU-bound (v_mad_u64_u32): see roofline_valu"},
+            "roofline_valu": {"kernel": "k_accumulate<G1>", "bound": "valu",
+                              "achieved": round(mad_t, 3) if mad_t else None, "peak": MAD_RATE_T,
+                              "unit": "T v_mad_u64_u32/s", "frac": round(mad_t / MAD_RATE_T, 4) if mad_t else None,
+                              "mads_per_launch": contributions * MADS_PER_G1_MADD,
+                              "note": f"{contributions} mixed additions x {MADS_PER_G1_MADD} mads "
+                                      "(algorithmic); peak = measured mad issue rate"},
             "roofline_ntt": {"kernel": "k_ntt_pass x passes (one transform)", "bound": "hbm",
                              "achieved": round(ntt_ach, 2) if ntt_ach else None, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(ntt_ach / HBM_PEAK_GBS, 5) if ntt_ach else None,
                              "traffic": ntt_traffic(args.ntt_log),
-                             "traffic_source": "profiles/r01/pmc_summary.json (first + middle + last pass)",
+                             "valu_frac": round(ntt_mad_t / MAD_RATE_T, 4) if ntt_mad_t else None,
                              "pass_ms": round(ntt_pass_ms, 4) if ntt_pass_ms else None},
+            "config4_msm_sharded": cfg4,
             "cpu_baseline": cpu,
         }
+        out.update(extra)
+        out.update(legs)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_over_ranks, world):
+    """the same 2^20 G1 MSM through the reference's raw entry, host-staged scalars, and the
+    batched ICICLE call (rank-local: no exchange)"""
+    out = {}
+    res = torch.zeros((1, 18), dtype=torch.int64, device=dev)
+    reps = max(3, args.steps // 2)
+    # the reference's raw entry bls12_381_g1_msm_cuda (icicle_curve_api.cu:679): standard scalars,
+    # Jacobian Montgomery result, no normalisation (round 1's headline)
+    s_std = torch.zeros_like(scalars)
+    amd.gen_scalars(s_std, 0x5EED0003, montgomery=False, stream=stream)
+    raw_ms = max_over_ranks(timed(lambda: amd.msm("g1", s_std, bases, icicle=False, out=res, stream=stream,
+                                                  is_async=True, n=n), reps))
+    out["msm_raw_entry_per_sec"] = round(world * 1e3 / raw_ms, 3)
+    del s_std
+    # host-inclusive: scalars in pinned host memory, staged by the call (BASELINE.md 2: end-to-end
+    # rate with the scalar H2D; never `value`)
+    host_s = scalars.cpu().pin_memory()
+    torch.cuda.synchronize(dev)
+    hi_ms = max_over_ranks(timed(lambda: amd.msm("g1", host_s, bases, icicle=True, scalars_mont=True, out=res,
+                                                 stream=stream, is_async=True, n=n), reps))
+    out["msm_host_scalars_per_sec"] = round(world * 1e3 / hi_ms, 3)
+    del host_s
+    # batched MSMs (ICICLE batch_size, shared device bases): members pipelined on two streams
+    if args.msm_batch > 1:
+        B = args.msm_batch
+        sb = torch.zeros((B * n, 4), dtype=torch.int64, device=dev)
+        amd.gen_scalars(sb, 0x5EED0033, montgomery=True, stream=stream)
+        rb = torch.zeros((B, 18), dtype=torch.int64, device=dev)
+        breps = max(2, args.steps // 4)
+        b_ms = max_over_ranks(timed(lambda: amd.msm("g1", sb, bases, icicle=True, scalars_mont=True, batch=B,
+                                                    out=rb, stream=stream, is_async=True, n=n), breps))
+        out["msm_batch"] = {"batch": B, "reps": breps, "ms_per_batch": round(b_ms, 3),
+                            "msm_per_sec": round(world * B * 1e3 / b_ms, 3),
+                            "note": "ICICLE batch_size (core/msm.rs msm_batch_with_device_bases), members "
+                                    "pipelined on two HIP streams"}
+        del sb
+    return out
+
+
+def vecops_leg(amd, torch, dev, stream, timed):
+    """config #1 on the GPU: vector add / mul at 2^16 (launch-bound) and 2^24 (HBM roofline)"""
+    out = {}
+    for log_n in (16, 24):
+        n = 1 << log_n
+        a = torch.zeros((n, 4), dtype=torch.int64, device=dev)
+        b = torch.zeros_like(a)
+        c = torch.zeros_like(a)
+        amd.gen_scalars(a, 0x5EED0001, montgomery=True, stream=stream)
+        amd.gen_scalars(b, 0x5EED0101, montgomery=True, stream=stream)
+        for op in ("add", "mul"):
+            reps = 200 if log_n == 16 else 20
+            ms = timed(lambda: amd.vec_op(op, a, b, out=c, stream=stream, is_async=True), reps, warm=3)
+            gbs = VEC_BYTES_PER_ELEM * n / (ms * 1e-3) / 1e9
+            out[f"{op}_2^{log_n}"] = {"ms": round(ms, 5), "gb_per_s": round(gbs, 1),
+                                      "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+        del a, b, c
+    out["note"] = "96 B/elem algorithmic; wall time per call (host launch included at 2^16)"
+    return out
 
 
 def ntt_traffic(log_n):
     """HBM bytes of one forward 2^22 transform: first + middle + last pass (pmc_probe sizes)"""
     if log_n != 22:
         return None
-    parts = [pmc_traffic(k) for k in ("k_ntt_pass<true, false, false>", "k_ntt_pass<false, false, false>",
-                                      "k_ntt_pass<false, true, false>")]
+    names = ("k_ntt_pass<true, false, false>", "k_ntt_pass<false, false, false>", "k_ntt_pass<false, true, false>")
+    parts = [pmc_traffic(k) for k in names]
     return None if any(p is None for p in parts) else sum(parts)
 
 
-def mix_leg(args, amd, torch, dev, rank):
-    """BASELINE config #5: G2 MSM 2^msm_log and a batch of Fr NTTs 2^ntt_log enqueued on two
-    HIP streams at once (PLONK-prover-shaped mix); reports each alone and the overlapped wall."""
+def mix_leg(args, amd, torch, dev, rank, timed):
+    """BASELINE config #5: G2 MSM 2^msm_log (ICICLE entry) and a batch of Fr NTTs 2^ntt_log
+    enqueued on two HIP streams at once (PLONK-prover-shaped mix); each alone and overlapped."""
     n = 1 << args.msm_log
     nn = 1 << args.ntt_log
     B = args.mix_batch
@@ -275,45 +379,40 @@ def mix_leg(args, amd, torch, dev, rank):
     s_b = torch.cuda.Stream(dev)
     sc = torch.zeros((n, 4), dtype=torch.int64, device=dev)
     bs = torch.zeros((n, 24), dtype=torch.int64, device=dev)
-    amd.gen_scalars(sc, 0x5EED0005 + rank, montgomery=True, stream=s_a)
-    amd.gen_bases("g2", bs, 0x5EED0015 + rank, stream=s_a)
+    amd.gen_scalars(sc, 0x5EED0005, montgomery=True, stream=s_a)
+    amd.gen_bases("g2", bs, 0x5EED0015, stream=s_a)
     res = torch.zeros((1, 36), dtype=torch.int64, device=dev)
     xb = torch.zeros((B * nn, 4), dtype=torch.int64, device=dev)
     yb = torch.zeros_like(xb)
-    amd.gen_scalars(xb, 0x5EED0025 + rank, montgomery=True, stream=s_b)
+    amd.gen_scalars(xb, 0x5EED0025, montgomery=True, stream=s_b)
     torch.cuda.synchronize(dev)
 
     def g2():
-        amd.msm("g2", sc, bs, icicle=False, scalars_mont=True, out=res, stream=s_a, is_async=True, n=n)
+        amd.msm("g2", sc, bs, icicle=True, scalars_mont=True, out=res, stream=s_a, is_async=True, n=n)
 
     def ntts():
         amd.ntt(xb, out=yb, batch=B, stream=s_b, is_async=True)
-
-    def timed(fn, reps):
-        fn()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            fn()
-        torch.cuda.synchronize(dev)
-        return (time.perf_counter() - t0) / reps * 1e3
 
     reps = max(2, min(args.steps, 5))
     g2_ms = timed(g2, reps)
     ntt_ms = timed(ntts, reps)
     both_ms = timed(lambda: (g2(), ntts()), reps)
     return {"g2_msm_points": n, "ntt_batch": B, "ntt_size": nn, "g2_msm_ms": round(g2_ms, 3),
-            "g2_msm_per_sec": round(1e3 / g2_ms, 3), "batched_ntt_ms": round(ntt_ms, 3),
-            "overlapped_ms": round(both_ms, 3), "sum_isolated_ms": round(g2_ms + ntt_ms, 3),
-            "streams": 2}
+            "g2_msm_per_sec": round(1e3 / g2_ms, 3),
+            "g2_roofline_hbm_frac": round(G2_BYTES_PER_POINT * n / (g2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "batched_ntt_ms": round(ntt_ms, 3), "overlapped_ms": round(both_ms, 3),
+            "sum_isolated_ms": round(g2_ms + ntt_ms, 3), "streams": 2,
+            "g2_result_digest": digest(res)}
 
 
-def cpu_baseline(args, amd, scalars, bases, n):
-    """The oracle (C port of the reference CPU semantics, multithreaded Pippenger) on the
-    host cores, on the same 2^msm_log inputs copied back from the device."""
-    import ctypes
+def cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, ntt_in):
+    """The oracle (oracle/bls12_381_oracle.c: C restatement of the reference CPU semantics,
+    OpenMP Pippenger / radix-2 NTT / vecops) on the host cores, on the SAME inputs as the GPU
+    legs.  MSM: median of repeated full 2^msm_log runs within --cpu-budget-s, and the result
+    must equal the GPU headline result (bit_exact).  BLST is not available."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import gpu_helpers
     import helpers as H
     o = H.oracle()
     threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
@@ -324,12 +423,55 @@ def cpu_baseline(args, amd, scalars, bases, n):
     one = np.zeros((n, 4), dtype=np.uint64)
     one[:, 0] = 1
     o.orc_vec_mul(H.ptr(s_std), H.ptr(s_mont), H.ptr(one), n)
-    t0 = time.perf_counter()
-    H.oracle_msm("g1", s_std, b, threads=threads)
-    t = time.perf_counter() - t0
-    return {"value": round(1.0 / t, 4), "unit": "MSM/s", "cores": threads, "kind": "port",
-            "sample": f"one full G1 MSM of 2^{args.msm_log} points (same inputs), oracle/bls12_381_oracle.c "
-                      f"multithreaded Pippenger, {threads} threads; BLST not available"}
+    times, ref = [], None
+    t_start = time.perf_counter()
+    while len(times) < 5 and (len(times) < 2 or time.perf_counter() - t_start < args.cpu_budget_s):
+        t0 = time.perf_counter()
+        ref = H.oracle_msm("g1", s_std, b, threads=threads)
+        times.append(time.perf_counter() - t0)
+    msm_s = statistics.median(times)
+    got = gpu_helpers.decode_icicle("g1", amd.to_numpy_u64(headline_result)[0])
+    bit_exact = got == H.g1_from_affine_mont(ref)
+    out = {"value": round(1.0 / msm_s, 4), "unit": "MSM/s", "cores": threads, "kind": "port",
+           "sample": f"full G1 MSM of 2^{args.msm_log} points on the headline's inputs, median of {len(times)} "
+                     f"runs, oracle/bls12_381_oracle.c OpenMP Pippenger on {threads} threads; BLST not available",
+           "bit_exact": bool(bit_exact)}
+    # NTT (config #2 / the metric's second half): oracle radix-2 best_fft, all threads
+    xn = np.ascontiguousarray(amd.to_numpy_u64(ntt_in))
+    for log_n in (20, args.ntt_log):
+        a = np.ascontiguousarray(xn[: 1 << log_n])
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            H.oracle_ntt(a, log_n, False, threads=threads)
+            ts.append(time.perf_counter() - t0)
+        out[f"ntt_2^{log_n}_ms"] = round(statistics.median(ts) * 1e3, 2)
+    # vecops 2^16 (config #1: the CPU path of MIDNIGHT_DEVICE=cpu, core/vecops.rs:575-610)
+    va = np.ascontiguousarray(xn[: 1 << 16])
+    vb = np.ascontiguousarray(xn[1 << 16: 2 << 16])
+    vc = np.zeros_like(va)
+    for th, tag in ((1, "1t"), (threads, f"{threads}t")):
+        o.orc_set_threads(th)
+        for op, fn in (("add", o.orc_vec_add), ("mul", o.orc_vec_mul)):
+            ts = []
+            for _ in range(20):
+                t0 = time.perf_counter()
+                fn(H.ptr(vc), H.ptr(va), H.ptr(vb), 1 << 16)
+                ts.append(time.perf_counter() - t0)
+            out[f"vec_{op}_2^16_{tag}_us"] = round(statistics.median(ts) * 1e6, 1)
+    o.orc_set_threads(0)
+    # G2 MSM (config #5): one full 2^msm_log run on the mix leg's inputs
+    if not args.no_mix:
+        g2s = torch.zeros((n, 4), dtype=torch.int64, device=scalars.device)
+        g2b = torch.zeros((n, 24), dtype=torch.int64, device=scalars.device)
+        amd.gen_scalars(g2s, 0x5EED0005, montgomery=False)
+        amd.gen_bases("g2", g2b, 0x5EED0015)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        H.oracle_msm("g2", np.ascontiguousarray(amd.to_numpy_u64(g2s)), np.ascontiguousarray(amd.to_numpy_u64(g2b)),
+                     threads=threads)
+        out[f"g2_msm_2^{args.msm_log}_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+    return out
 
 
 if __name__ == "__main__":

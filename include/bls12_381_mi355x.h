@@ -145,8 +145,15 @@ eIcicleError bls12_381_icicle_g1_msm(const mbls_fr_t* scalars, const mbls_g1_aff
 eIcicleError bls12_381_icicle_g2_msm(const mbls_fr_t* scalars, const mbls_g2_affine_t* bases, int msm_size,
                                      const MSMConfig* config, mbls_g2_projective_t* results);
 
-/* precompute_bases, reference icicle_curve_api.cu:415-440: factor 1 only (byte copy);
- * factor > 1 returns MBLS_API_NOT_IMPLEMENTED rather than silently wrong data.           */
+/* precompute_bases, reference icicle_curve_api.cu:415-440 (there a plain byte copy, so its
+ * factor > 1 gives wrong MSMs).  Here factor F = config->precompute_factor in 1..64 writes the
+ * point-major table out[i*F + f] = 2^(s*f) * P_i with s = ceil(256 / F) (core/msm.rs:164-165):
+ * the shift depends on F only, so ONE table serves MSMs of any c (config->c is ignored here)
+ * and any msm_size <= bases_size.  Output: Montgomery affine; standard-form input
+ * (are_points_montgomery_form = false) is converted first.  An MSM with precompute_factor
+ * F > 1 reads such a table (n*F entries, the full buffer may be passed) and treats it as
+ * Montgomery whatever are_points_montgomery_form says -- core/msm.rs:641-643 passes false
+ * with a precomputed table.                                                               */
 eIcicleError bls12_381_icicle_g1_msm_precompute_bases(const mbls_g1_affine_t* input_bases, int bases_size,
                                                       const MSMConfig* config, mbls_g1_affine_t* output_bases);
 eIcicleError bls12_381_icicle_g2_msm_precompute_bases(const mbls_g2_affine_t* input_bases, int bases_size,
@@ -215,6 +222,21 @@ eIcicleError mbls_gen_scalars(mbls_fr_t* out_device, uint64_t seed, size_t n, bo
 /* Fill `out` (device) with P_i = k_i * G, k_i = scalar stream `seed` (affine Montgomery). */
 eIcicleError mbls_gen_g1_bases(mbls_g1_affine_t* out_device, uint64_t seed, size_t n, void* stream);
 eIcicleError mbls_gen_g2_bases(mbls_g2_affine_t* out_device, uint64_t seed, size_t n, void* stream);
+/* The same streams from element `start` on (out[j] = element start + j): one rank of a sharded
+ * run generates exactly its slice of the global inputs. */
+eIcicleError mbls_gen_scalars_range(mbls_fr_t* out_device, uint64_t seed, size_t start, size_t n, bool montgomery,
+                                    void* stream);
+eIcicleError mbls_gen_g1_bases_range(mbls_g1_affine_t* out_device, uint64_t seed, size_t start, size_t n, void* stream);
+eIcicleError mbls_gen_g2_bases_range(mbls_g2_affine_t* out_device, uint64_t seed, size_t start, size_t n, void* stream);
+/* One rank's step of the sharded multi-GPU MSM (the reference has no
+ * multi-GPU path): the inputs and flags of bls12_381_icicle_g*_msm, but the result is left
+ * as the Jacobian Montgomery partial sum (no (x, y, 1) normalisation), so the partials of all
+ * ranks can be all-gathered, added with mbls_g*_sum_jacobian and normalised once with
+ * mbls_g*_jacobian_to_icicle. */
+eIcicleError mbls_g1_msm_jacobian(const mbls_fr_t* scalars, const mbls_g1_affine_t* bases, int msm_size,
+                                  const MSMConfig* config, mbls_g1_projective_t* results);
+eIcicleError mbls_g2_msm_jacobian(const mbls_fr_t* scalars, const mbls_g2_affine_t* bases, int msm_size,
+                                  const MSMConfig* config, mbls_g2_projective_t* results);
 /* Sum `count` Jacobian-Montgomery points on device (the EC reduction after the multi-GPU
  * all-gather of partial MSM results). result: device pointer, Jacobian Montgomery. */
 eIcicleError mbls_g1_sum_jacobian(const mbls_g1_projective_t* points_device, int count,

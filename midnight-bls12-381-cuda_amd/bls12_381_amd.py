@@ -70,6 +70,8 @@ EXPORTED = [
     "bls12_381_scalar_add_vec", "vec_add_cuda", "vec_sub_cuda", "vec_mul_cuda", "scalar_mul_vec_cuda",
     "scalar_add_vec_cuda", "vec_sum_cuda", "bls12_381_batch_inv_cuda",
     "mbls_version", "mbls_error_string", "mbls_gen_scalars", "mbls_gen_g1_bases", "mbls_gen_g2_bases",
+    "mbls_gen_scalars_range", "mbls_gen_g1_bases_range", "mbls_gen_g2_bases_range",
+    "mbls_g1_msm_jacobian", "mbls_g2_msm_jacobian",
     "mbls_g1_sum_jacobian", "mbls_g2_sum_jacobian", "mbls_g1_jacobian_to_icicle", "mbls_g2_jacobian_to_icicle",
     "mbls_profile_enable", "mbls_profile_reset", "mbls_profile_read",
 ]
@@ -104,6 +106,9 @@ def lib():
         "vec_sum_cuda": [P, P, i32, P], "bls12_381_batch_inv_cuda": [P, P, i32, P],
         "mbls_gen_scalars": [P, u64, sz, b, P], "mbls_gen_g1_bases": [P, u64, sz, P],
         "mbls_gen_g2_bases": [P, u64, sz, P], "mbls_g1_sum_jacobian": [P, i32, P, P],
+        "mbls_gen_scalars_range": [P, u64, sz, sz, b, P], "mbls_gen_g1_bases_range": [P, u64, sz, sz, P],
+        "mbls_gen_g2_bases_range": [P, u64, sz, sz, P],
+        "mbls_g1_msm_jacobian": [P, P, i32, P, P], "mbls_g2_msm_jacobian": [P, P, i32, P, P],
         "mbls_g2_sum_jacobian": [P, i32, P, P], "mbls_g1_jacobian_to_icicle": [P, i32, P],
         "mbls_g2_jacobian_to_icicle": [P, i32, P],
     }
@@ -159,7 +164,9 @@ def _p(x):
 
 
 def _is_dev(x):
-    return x is not None and not isinstance(x, np.ndarray)
+    """device operand: a torch tensor on the GPU (numpy arrays and CPU / pinned torch tensors
+    are host memory)"""
+    return x is not None and not isinstance(x, np.ndarray) and bool(getattr(x, "is_cuda", True))
 
 
 def _stream_handle(stream):
@@ -270,7 +277,9 @@ def ntt(x, inverse=False, out=None, batch=1, stream=None, is_async=False, coset_
 def msm(group, scalars, bases, *, icicle=True, scalars_mont=False, points_mont=True, c=0, bitsize=0,
         precompute_factor=1, batch=1, shared_bases=True, out=None, stream=None, is_async=False, n=None):
     """scalars (batch*n, 4) u64, bases (n*F[*batch], 12|24) u64; host numpy or device torch.
-    icicle=True -> ICICLE semantics (standard (x, y, 1)); False -> raw Jacobian Montgomery."""
+    icicle=True -> ICICLE semantics (standard (x, y, 1)); False -> the reference's raw entry
+    (standard scalars, Jacobian Montgomery); "jacobian" -> ICICLE inputs, Jacobian Montgomery
+    result (one rank's step of the sharded MSM)."""
     nl = 18 if group == "g1" else 36
     if n is None:
         n = scalars.shape[0] // batch
@@ -281,7 +290,9 @@ def msm(group, scalars, bases, *, icicle=True, scalars_mont=False, points_mont=T
                      are_scalars_montgomery_form=scalars_mont, are_points_on_device=_is_dev(bases),
                      are_points_montgomery_form=points_mont, are_results_on_device=_is_dev(out),
                      is_async=is_async, stream=stream)
-    if icicle:
+    if icicle == "jacobian":
+        fn = lib().mbls_g1_msm_jacobian if group == "g1" else lib().mbls_g2_msm_jacobian
+    elif icicle:
         fn = lib().bls12_381_icicle_g1_msm if group == "g1" else lib().bls12_381_icicle_g2_msm
     else:
         fn = lib().bls12_381_g1_msm_cuda if group == "g1" else lib().bls12_381_g2_msm_cuda
@@ -289,12 +300,14 @@ def msm(group, scalars, bases, *, icicle=True, scalars_mont=False, points_mont=T
     return out
 
 
-def precompute_bases(group, bases, factor, n, c=0, out=None):
+def precompute_bases(group, bases, factor, n, c=0, out=None, points_mont=True):
+    """ICICLE precompute_bases: out[i*factor + f] = 2^(s f) P_i, s = ceil(256 / factor) (the
+    shift depends on the factor only, so c is irrelevant); output Montgomery affine."""
     nl = 12 if group == "g1" else 24
     if out is None:
         out = np.zeros((n * factor, nl), dtype=np.uint64)
     cfg = msm_config(precompute_factor=factor, c=c, are_points_on_device=_is_dev(bases),
-                     are_points_montgomery_form=True, are_results_on_device=_is_dev(out))
+                     are_points_montgomery_form=points_mont, are_results_on_device=_is_dev(out))
     fn = (lib().bls12_381_icicle_g1_msm_precompute_bases if group == "g1"
           else lib().bls12_381_icicle_g2_msm_precompute_bases)
     check(fn(_p(bases), n, ctypes.byref(cfg), _p(out)), "precompute_bases")
@@ -302,14 +315,15 @@ def precompute_bases(group, bases, factor, n, c=0, out=None):
 
 
 # ----------------------------------------------------------------------------- utilities
-def gen_scalars(out_dev, seed, montgomery=False, stream=None):
-    check(lib().mbls_gen_scalars(_p(out_dev), seed, out_dev.shape[0], montgomery, _stream_handle(stream)),
-          "gen_scalars")
+def gen_scalars(out_dev, seed, montgomery=False, stream=None, start=0):
+    """elements start .. start + len(out_dev) - 1 of scalar stream `seed`"""
+    check(lib().mbls_gen_scalars_range(_p(out_dev), seed, start, out_dev.shape[0], montgomery,
+                                       _stream_handle(stream)), "gen_scalars")
 
 
-def gen_bases(group, out_dev, seed, stream=None):
-    fn = lib().mbls_gen_g1_bases if group == "g1" else lib().mbls_gen_g2_bases
-    check(fn(_p(out_dev), seed, out_dev.shape[0], _stream_handle(stream)), "gen_bases")
+def gen_bases(group, out_dev, seed, stream=None, start=0):
+    fn = lib().mbls_gen_g1_bases_range if group == "g1" else lib().mbls_gen_g2_bases_range
+    check(fn(_p(out_dev), seed, start, out_dev.shape[0], _stream_handle(stream)), "gen_bases")
 
 
 def sum_jacobian(group, pts_dev, out_dev, stream=None):

@@ -95,10 +95,22 @@ enum class eIcicleError {
     UNKNOWN_ERROR = 14
 };
 
+// ICICLE's device descriptor (vendored include/icicle/device.h:55-57): the type string is an
+// inline char[32], so `id` sits at byte offset 32 (the reference's icicle_types.cuh:69-72
+// declares {const char*, int}, which reads `id` from inside the string)
 struct Device {
-    const char* type;
+    char type[32];
     int id;
 };
+static_assert(offsetof(Device, id) == 32 && sizeof(Device) == 36, "icicle::Device layout (device.h:55-57)");
+// what ICICLE's Device(const char*, int) constructor produces (zero-padded, truncated type)
+inline Device make_device(const char* type, int id) {
+    Device d;
+    for (size_t i = 0; i < sizeof d.type; ++i) d.type[i] = 0;
+    for (size_t i = 0; type && type[i] && i + 1 < sizeof d.type; ++i) d.type[i] = type[i];
+    d.id = id;
+    return d;
+}
 
 typedef void* icicleStreamHandle;
 
@@ -194,8 +206,10 @@ void register_g2_msm_precompute_bases(const std::string& deviceType, MsmG2PreCom
 MsmG2Impl get_g2_msm_backend(const std::string& deviceType);
 MsmG2PreComputeImpl get_g2_precompute_backend(const std::string& deviceType);
 
-// ---- device API (reference cuda_device_api.cu:38-149; virtual order = its override order) ----
-enum class eCopyDirection { HostToDevice = 0, DeviceToHost = 1, DeviceToDevice = 2 };
+// ---- device API (vtable order of the vendored include/icicle/device_api.h:52-131, which the
+//      reference's cuda_device_api.cu:38-149 overrides) ----
+// device_api.h:44 (plain enum there; same int values)
+enum class eCopyDirection { HostToDevice = 0, DeviceToHost = 1, DeviceToDevice = 2, HostToHost = 3 };
 struct DeviceProperties {
     bool using_host_memory;
     int num_memory_regions;

@@ -112,7 +112,7 @@ extern "C" ::eIcicleError mbls_icicle_g2_msm_via_registry(const char* device_typ
                                                           mbls_g2_projective_t* results) {
     auto impl = icicle::get_g2_msm_backend(device_type ? device_type : "");
     if (!impl || !cfg) return MBLS_INVALID_ARGUMENT;
-    icicle::Device d{device_type, 0};
+    const icicle::Device d = icicle::make_device(device_type, 0);
     return static_cast<::eIcicleError>(static_cast<int>(
         impl(d, reinterpret_cast<const icicle::scalar_t*>(scalars), reinterpret_cast<const icicle::g2_affine_t*>(bases), n,
              *reinterpret_cast<const icicle::MSMConfig*>(cfg), reinterpret_cast<icicle::g2_projective_t*>(results))));

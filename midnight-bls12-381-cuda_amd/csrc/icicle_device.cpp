@@ -28,9 +28,12 @@ using icicle::backend_device_type;
 using namespace icicle;  // register_* (no clashes: the C ABI has no such names)
 
 hipMemcpyKind kind(eCopyDirection d) {
-    return d == eCopyDirection::HostToDevice   ? hipMemcpyHostToDevice
-           : d == eCopyDirection::DeviceToHost ? hipMemcpyDeviceToHost
-                                               : hipMemcpyDeviceToDevice;
+    switch (d) {
+        case eCopyDirection::HostToDevice: return hipMemcpyHostToDevice;
+        case eCopyDirection::DeviceToHost: return hipMemcpyDeviceToHost;
+        case eCopyDirection::HostToHost: return hipMemcpyHostToHost;
+        default: return hipMemcpyDeviceToDevice;
+    }
 }
 hipStream_t hs(icicleStreamHandle s) { return static_cast<hipStream_t>(s); }
 eIcicleError ok_or(hipError_t e, eIcicleError fail) { return e == hipSuccess ? eIcicleError::SUCCESS : fail; }
@@ -38,6 +41,9 @@ eIcicleError ok_or(hipError_t e, eIcicleError fail) { return e == hipSuccess ? e
 class HipDeviceAPI final : public DeviceAPI {
    public:
     eIcicleError set_device(const Device& device) override {
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || device.id < 0 || device.id >= count)
+            return eIcicleError::INVALID_DEVICE;
         return ok_or(hipSetDevice(device.id), eIcicleError::INVALID_DEVICE);
     }
     eIcicleError get_device_count(int& device_count) const override {

@@ -22,6 +22,8 @@ static int optimal_c(long long n) {
     return 16;
 }
 
+int precompute_shift(int F) { return F > 1 ? (256 + F - 1) / F : 0; }
+
 eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) {
     int c = cfg->c > 0 ? cfg->c : optimal_c(n);
     if (c < 2 || c > 20) return MBLS_INVALID_ARGUMENT;
@@ -35,10 +37,19 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     p.split = 1;
     if (endo == 2 && F == 1 && bits > 128) p.split = 2;
     if (endo == 4 && F == 1 && bits > 192 && c <= 16) p.split = 4;
+    if (F > MAX_PRECOMPUTE) return MBLS_INVALID_ARGUMENT;
     // signed digits need one bit of headroom for the top carry
     int W = p.split == 2 ? (128 + c - 1) / c : p.split == 4 ? (64 + c - 1) / c : (bits + 1 + c - 1) / c;
-    if (F > W) F = W;
-    int Wg = (W + F - 1) / F;
+    int Wg = W;
+    p.sF = 0;
+    if (F > 1) {
+        // precomputed bases: the table's shift depends on F only (precompute_shift), so the
+        // table serves every c and msm_size (core/msm.rs:441-454 precomputes with c = 0, the MSM
+        // may run with MIDNIGHT_MSM_WINDOW); blocks of sF bits, Wg windows each, all 256 bits
+        p.sF = precompute_shift(F);
+        Wg = (p.sF + c - 1) / c;
+        W = F * Wg;
+    }
     p.c = c;
     p.W = W;
     p.F = F;
@@ -111,11 +122,28 @@ MBLS_DEV void emit_digit(uint32_t key, uint32_t val, size_t o, uint32_t* __restr
     }
 }
 
+// Window geometry.  sF == 0: uniform windows, window j = bits [c j, c j + c).  sF > 0
+// (precomputed bases, factor F): the scalar is cut into F blocks of sF = ceil(256 / F) bits,
+// block f multiplies table entry i*F + f = 2^(sF f) P_i, and holds Wg = ceil(sF / c) windows;
+// window j = f Wg + l covers bits [sF f + c l, sF f + min(c (l + 1), sF)) -- the block's last
+// window is narrower when c does not divide sF.  The signed-digit carry runs through all
+// windows in order; a window of width < c never carries (its value + carry <= 2^(c-1) = B).
+MBLS_DEV void window_span(int j, int c, int Wg, int sF, int& pos, int& wid) {
+    if (sF == 0) {
+        pos = j * c;
+        wid = c;
+        return;
+    }
+    const int f = j / Wg, l = j - f * Wg;
+    pos = sF * f + c * l;
+    wid = min(c, sF - c * l);
+}
+
 // ------------------------------------------------------------------------------------
 // 1. digits: one thread per scalar
 // ------------------------------------------------------------------------------------
 template <bool MONT>
-__global__ __launch_bounds__(256) void k_digits(const uint8_t* __restrict__ scalars, uint32_t n, int c, int W, int Wg, uint32_t F,
+__global__ __launch_bounds__(256) void k_digits(const uint8_t* __restrict__ scalars, uint32_t n, int c, int W, int Wg, int sF, uint32_t F,
                                                 uint32_t B, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                 uint32_t* __restrict__ ranks, uint32_t* __restrict__ counts) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -123,9 +151,10 @@ __global__ __launch_bounds__(256) void k_digits(const uint8_t* __restrict__ scal
     Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
     if (MONT) s = from_mont(s);
     uint32_t carry = 0;
-    const uint32_t mask = (1u << c) - 1;
     for (int w = 0; w < W; ++w) {
-        const int bit = w * c;
+        int bit, wid;
+        window_span(w, c, Wg, sF, bit, wid);
+        const uint32_t mask = (1u << wid) - 1;
         const int word = bit >> 5, sh = bit & 31;
         // select words without dynamic register indexing (which would go to scratch)
         uint32_t lo = 0, hi = 0;
@@ -483,11 +512,11 @@ __global__ void k_scalars_std(const uint8_t* __restrict__ scalars, uint32_t n, u
 
 // signed digit of window w (carry chain from window 0), magnitude in v, sign in bit 31
 template <int NW>
-MBLS_DEV uint32_t digit_at(const uint32_t (&x)[NW], int w, int c, uint32_t B) {
-    const uint32_t mask = (1u << c) - 1;
+MBLS_DEV uint32_t digit_at(const uint32_t (&x)[NW], int w, int c, uint32_t B, int Wg, int sF) {
     uint32_t carry = 0, v = 0;
     for (int j = 0; j <= w; ++j) {
-        const int bit = j * c;
+        int bit, wid;
+        window_span(j, c, Wg, sF, bit, wid);
         const int word = bit >> 5, sh = bit & 31;
         uint32_t lo = 0, hi = 0;
 #pragma unroll
@@ -495,7 +524,7 @@ MBLS_DEV uint32_t digit_at(const uint32_t (&x)[NW], int w, int c, uint32_t B) {
             lo = (k == word) ? x[k] : lo;
             hi = (k == word + 1) ? x[k] : hi;
         }
-        v = ((uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & mask) + carry;
+        v = ((uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & ((1u << wid) - 1)) + carry;
         carry = v > B ? 1u : 0u;
     }
     return carry ? (((1u << c) - v) | 0x80000000u) : v;
@@ -505,7 +534,7 @@ MBLS_DEV uint32_t digit_at(const uint32_t (&x)[NW], int w, int c, uint32_t B) {
 // plain: indices [0, n) over scalars, vals ((i*F + w/Wg) << 1 | sign), key (w%Wg)*B + v - 1.
 template <bool GLV>
 __global__ __launch_bounds__(DT_THREADS) void k_digits_tiled(const uint32_t* __restrict__ src, uint32_t nidx, int c,
-                                                             int Wg, uint32_t F, uint32_t B,
+                                                             int Wg, int sF, uint32_t F, uint32_t B,
                                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                              uint32_t* __restrict__ ranks, uint32_t* __restrict__ counts) {
     __shared__ uint32_t hist[DT_MAX_B];
@@ -538,7 +567,7 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_tiled(const uint32_t* __r
                 negh = x[3] >> 31;
                 x[3] &= 0x7fffffffu;
             }
-            const uint32_t d = digit_at<NW>(x, w, c, B) ^ (negh << 31);
+            const uint32_t d = digit_at<NW>(x, w, c, B, Wg, sF) ^ (negh << 31);
             dig[k] = d;
             if (d & 0x7fffffffu) lr[k] = atomicAdd(&hist[(d & 0x7fffffffu) - 1], 1u);
         }
@@ -607,10 +636,10 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
         const uint32_t tiles = (nidx + DT_TILE - 1) / DT_TILE;
         dim3 gt(tiles * (uint32_t)P.W);
         if (P.split > 1)  // GLV / psi sources share the sign-magnitude uint4 format
-            hipLaunchKernelGGL(k_digits_tiled<true>, gt, dim3(DT_THREADS), 0, st, src, nidx, P.c, P.Wg, (uint32_t)P.F,
+            hipLaunchKernelGGL(k_digits_tiled<true>, gt, dim3(DT_THREADS), 0, st, src, nidx, P.c, P.Wg, P.sF, (uint32_t)P.F,
                                P.B, keys, vals, ranks, counts);
         else
-            hipLaunchKernelGGL(k_digits_tiled<false>, gt, dim3(DT_THREADS), 0, st, src, nidx, P.c, P.Wg,
+            hipLaunchKernelGGL(k_digits_tiled<false>, gt, dim3(DT_THREADS), 0, st, src, nidx, P.c, P.Wg, P.sF,
                                (uint32_t)P.F, P.B, keys, vals, ranks, counts);
         MBLS_TRY(hipGetLastError());
         return MBLS_SUCCESS;
@@ -622,10 +651,10 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
         else
             hipLaunchKernelGGL(k_digits_glv<false>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.B, keys, vals, ranks, counts);
     } else if (mont)
-        hipLaunchKernelGGL(k_digits<true>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, (uint32_t)P.F, P.B, keys,
+        hipLaunchKernelGGL(k_digits<true>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, P.sF, (uint32_t)P.F, P.B, keys,
                            vals, ranks, counts);
     else
-        hipLaunchKernelGGL(k_digits<false>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, (uint32_t)P.F, P.B, keys,
+        hipLaunchKernelGGL(k_digits<false>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, P.sF, (uint32_t)P.F, P.B, keys,
                            vals, ranks, counts);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
@@ -757,7 +786,7 @@ PartSortSizes part_sort_sizes(const MsmPlan& P) {
 
 template <bool SPLIT, bool PACK>
 __global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __restrict__ src, uint32_t nidx, int c,
-                                                            int Wg, uint32_t F, uint32_t B, int FB, uint32_t NP,
+                                                            int Wg, int sF, uint32_t F, uint32_t B, int FB, uint32_t NP,
                                                             uint32_t* __restrict__ ent, uint32_t* __restrict__ seg_off,
                                                             uint32_t* __restrict__ seg_cnt,
                                                             uint32_t* __restrict__ part_tot) {
@@ -792,7 +821,7 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __re
                 negh = x[3] >> 31;
                 x[3] &= 0x7fffffffu;
             }
-            const uint32_t d = digit_at<NW>(x, w, c, B) ^ (negh << 31);
+            const uint32_t d = digit_at<NW>(x, w, c, B, Wg, sF) ^ (negh << 31);
             dig[k] = d;
             if (d & 0x7fffffffu) lr[k] = atomicAdd(&hist[((d & 0x7fffffffu) - 1) >> FB], 1u);
         }
@@ -929,7 +958,7 @@ eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, c
     dim3 g(z.segments), b(DT_THREADS);
     const uint32_t F = (uint32_t)P.F;
 #define MBLS_DP(S_, P_)                                                                                           \
-    hipLaunchKernelGGL((k_digits_part<S_, P_>), g, b, 0, st, src, nidx, P.c, P.Wg, F, P.B, z.FB, z.NP, ent, seg_off, \
+    hipLaunchKernelGGL((k_digits_part<S_, P_>), g, b, 0, st, src, nidx, P.c, P.Wg, P.sF, F, P.B, z.FB, z.NP, ent, seg_off, \
                        seg_cnt, part_tot)
     if (P.split > 1) {
         if (z.pack)
@@ -1048,10 +1077,10 @@ eIcicleError launch_scalars_from_mont(uint8_t* s, size_t n, hipStream_t st) {
     return MBLS_SUCCESS;
 }
 
-__global__ void k_gen_scalars(uint8_t* out, uint64_t seed, size_t n, int mont) {
+__global__ void k_gen_scalars(uint8_t* out, uint64_t seed, size_t start, size_t n, int mont) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Fr s = gen_scalar(seed, i);
+    Fr s = gen_scalar(seed, start + i);
     if (mont) s = to_mont(s);
     store<FrCfg>(out + 32 * i, s);
 }
@@ -1060,11 +1089,15 @@ __global__ void k_gen_scalars(uint8_t* out, uint64_t seed, size_t n, int mont) {
 
 using namespace mbls;
 
-extern "C" eIcicleError mbls_gen_scalars(mbls_fr_t* out_device, uint64_t seed, size_t n, bool montgomery, void* stream) {
+extern "C" eIcicleError mbls_gen_scalars_range(mbls_fr_t* out_device, uint64_t seed, size_t start, size_t n,
+                                               bool montgomery, void* stream) {
     if (!out_device) return MBLS_INVALID_POINTER;
     if (n == 0) return MBLS_SUCCESS;
     hipLaunchKernelGGL(k_gen_scalars, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       (uint8_t*)out_device, seed, n, montgomery ? 1 : 0);
+                       (uint8_t*)out_device, seed, start, n, montgomery ? 1 : 0);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
+}
+extern "C" eIcicleError mbls_gen_scalars(mbls_fr_t* out_device, uint64_t seed, size_t n, bool montgomery, void* stream) {
+    return mbls_gen_scalars_range(out_device, seed, 0, n, montgomery, stream);
 }

@@ -56,8 +56,11 @@ static constexpr int MAX_MSM_LOG = 26;
 static constexpr int SCAN_BLOCK = 1024;
 static constexpr int MAX_LEVELS = 16;
 
+static constexpr int MAX_PRECOMPUTE = 64;
+
 struct MsmPlan {
     int c, W, Wg, F;
+    int sF;                     // precomputed-table block shift in bits (0: F == 1), see window_span
     int split;                  // endomorphism split: 1 none, 2 G1 GLV (phi), 4 G2 psi
     uint32_t B, TB;
     size_t pts;                 // distinct point indices (n, n*F, or split*n)
@@ -76,6 +79,8 @@ struct MsmPlan {
 
 // endo: the split the group offers (1 none, 2 G1 GLV, 4 G2 psi); make_plan decides whether to use it
 eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo = 1);
+// bits between consecutive multiples in a precomputed table: [P, 2^s P, 2^(2s) P, ...], s = ceil(256 / F)
+int precompute_shift(int F);
 
 // ---- non-templated launchers (msm_common.hip) ----------------------------------------
 eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* keys,
@@ -542,10 +547,10 @@ MBLS_DEV Fr gen_scalar(uint64_t seed, uint64_t i) {
 
 // P_i = k_i * G (input generation only; not on the measured path)
 template <class F>
-__global__ void k_gen_bases(uint8_t* out, uint64_t seed, size_t n) {
+__global__ void k_gen_bases(uint8_t* out, uint64_t seed, size_t start, size_t n) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Fr k = gen_scalar(seed, i);
+    Fr k = gen_scalar(seed, start + i);
     Jacobian<F> g = Jacobian<F>::from_affine(generator<F>());
     store_affine<F>(out, i, jac_to_affine(jac_mul_u32(g, k.v)));
 }
@@ -857,9 +862,17 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
 // ------------------------------------------------------------------------------------
 // boundary wrappers (placement flags, Montgomery flags, batch, ICICLE result format)
 // ------------------------------------------------------------------------------------
+// entry-point semantics: RAW = the reference's bls12_381_g*_msm_cuda (standard scalars,
+// Montgomery bases, flags for placement only, Jacobian Montgomery result, one MSM); ICICLE =
+// msm_cuda_impl (Montgomery flags honoured, batch, (x, y, 1) standard result); JACOBIAN = ICICLE
+// inputs with the Jacobian Montgomery result left unnormalised (the per-rank step of the
+// sharded multi-GPU MSM: partials are summed before the one normalisation)
+enum MsmEntry : int { MSM_RAW = 0, MSM_ICICLE = 1, MSM_JACOBIAN = 2 };
+
 template <class F>
 eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, const MSMConfig* cfg, void* results,
-                      bool icicle_semantics) {
+                      int entry) {
+    const bool icicle_semantics = entry != MSM_RAW;
     constexpr size_t AFF = GroupTraits<F>::AFF, JAC = GroupTraits<F>::JAC;
     if (!cfg || !results) return MBLS_INVALID_POINTER;
     if (msm_size < 0 || msm_size > (1 << MAX_MSM_LOG)) return MBLS_INVALID_ARGUMENT;
@@ -870,7 +883,9 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     eIcicleError er = make_plan(msm_size > 0 ? msm_size : 1, cfg, P, std::is_same<F, Fq>::value ? 2 : 4);
     if (er != MBLS_SUCCESS) return er;
     const bool scal_mont = icicle_semantics ? cfg->are_scalars_montgomery_form : false;
-    const bool pts_mont = icicle_semantics ? cfg->are_points_montgomery_form : true;
+    // a precomputed table (F > 1) is precompute_call output, Montgomery whatever the flag says:
+    // core/msm.rs:641-643 passes are_bases_montgomery_form = !is_precomputed() = false with it
+    const bool pts_mont = icicle_semantics && P.F == 1 ? cfg->are_points_montgomery_form : true;
     const bool shared = cfg->are_points_shared_in_batch || batch == 1;
     const size_t n = (size_t)msm_size;
     const size_t nbases_per = n * (size_t)P.F;
@@ -941,7 +956,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
             if (er != MBLS_SUCCESS) return er;
         }
     }
-    if (icicle_semantics) {
+    if (entry == MSM_ICICLE) {
         hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch * 16 + 63) / 64), dim3(64), 0, st, d_r, batch);
         MBLS_TRY(hipGetLastError());
     }
@@ -952,17 +967,19 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     return MBLS_SUCCESS;
 }
 
+// ICICLE precompute_bases (registered MsmPreComputeImpl, icicle_backend_api.cuh:188-193; the
+// reference's icicle_curve_api.cu:415-440 is a plain byte copy, so its factor > 1 is wrong).
+// out[i*F + f] = 2^(s f) P_i, s = precompute_shift(F) = ceil(256 / F): the shift depends on the
+// factor only, so one table serves an MSM of any c (MIDNIGHT_MSM_WINDOW or auto) and any
+// msm_size <= bases_size, as core/msm.rs:441-454 -> :630-650 uses it.  The output is always
+// Montgomery affine; standard-form input (are_points_montgomery_form = false) is converted.
 template <class F>
 eIcicleError precompute_call(const void* in, int n, const MSMConfig* cfg, void* out) {
     constexpr size_t AFF = GroupTraits<F>::AFF;
     if (!cfg || !in || !out) return MBLS_INVALID_POINTER;
     if (n < 0) return MBLS_INVALID_ARGUMENT;
-    int factor = cfg->precompute_factor > 0 ? cfg->precompute_factor : 1;
-    MsmPlan P;
-    eIcicleError er = make_plan(n > 0 ? n : 1, cfg, P);
-    if (er != MBLS_SUCCESS) return er;
-    if (factor > P.W) return MBLS_INVALID_ARGUMENT;
-    if (!cfg->are_points_montgomery_form) return MBLS_API_NOT_IMPLEMENTED;
+    const int factor = cfg->precompute_factor > 0 ? cfg->precompute_factor : 1;
+    if (factor > MAX_PRECOMPUTE) return MBLS_INVALID_ARGUMENT;
     if (n == 0) return MBLS_SUCCESS;
     hipStream_t st = static_cast<hipStream_t>(cfg->stream);
     StreamCtx& ctx = stream_ctx(st);
@@ -970,13 +987,15 @@ eIcicleError precompute_call(const void* in, int n, const MSMConfig* cfg, void* 
     Arena& A = ctx.arena;
     A.reset();
     size_t in_b = (size_t)n * AFF, out_b = in_b * factor;
-    er = A.reserve(align_up(in_b) + align_up(out_b));
+    eIcicleError er = A.reserve(align_up(in_b) + align_up(out_b));
     if (er != MBLS_SUCCESS) return er;
     uint8_t* din = (uint8_t*)A.take(in_b);
     uint8_t* dout = (uint8_t*)A.take(out_b);
     MBLS_TRY(hipMemcpyAsync(din, in, in_b, cfg->are_points_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    if (!cfg->are_points_montgomery_form)
+        hipLaunchKernelGGL(k_points_to_mont<F>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, din, (size_t)n);
     hipLaunchKernelGGL(k_precompute<F>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, st, din, dout, (size_t)n, factor,
-                       P.c * P.Wg);
+                       precompute_shift(factor));
     MBLS_TRY(hipGetLastError());
     MBLS_TRY(hipMemcpyAsync(out, dout, out_b, cfg->are_results_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
     MBLS_TRY(hipStreamSynchronize(st));

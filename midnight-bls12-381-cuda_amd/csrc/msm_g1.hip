@@ -10,23 +10,30 @@ extern "C" {
 
 eIcicleError bls12_381_g1_msm_cuda(const mbls_fr_t* scalars, const mbls_g1_affine_t* bases, int msm_size,
                                    const MSMConfig* config, mbls_g1_projective_t* result) {
-    return msm_call<G>(scalars, bases, msm_size, config, result, false);
+    return msm_call<G>(scalars, bases, msm_size, config, result, MSM_RAW);
 }
 eIcicleError bls12_381_icicle_g1_msm(const mbls_fr_t* scalars, const mbls_g1_affine_t* bases, int msm_size,
                                      const MSMConfig* config, mbls_g1_projective_t* results) {
-    return msm_call<G>(scalars, bases, msm_size, config, results, true);
+    return msm_call<G>(scalars, bases, msm_size, config, results, MSM_ICICLE);
 }
 eIcicleError bls12_381_icicle_g1_msm_precompute_bases(const mbls_g1_affine_t* input_bases, int bases_size,
                                                       const MSMConfig* config, mbls_g1_affine_t* output_bases) {
     return precompute_call<G>(input_bases, bases_size, config, output_bases);
 }
-eIcicleError mbls_gen_g1_bases(mbls_g1_affine_t* out_device, uint64_t seed, size_t n, void* stream) {
+eIcicleError mbls_gen_g1_bases_range(mbls_g1_affine_t* out_device, uint64_t seed, size_t start, size_t n, void* stream) {
     if (!out_device) return MBLS_INVALID_POINTER;
     if (n == 0) return MBLS_SUCCESS;
     hipLaunchKernelGGL(k_gen_bases<G>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, (hipStream_t)stream,
-                       (uint8_t*)out_device, seed, n);
+                       (uint8_t*)out_device, seed, start, n);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
+}
+eIcicleError mbls_gen_g1_bases(mbls_g1_affine_t* out_device, uint64_t seed, size_t n, void* stream) {
+    return mbls_gen_g1_bases_range(out_device, seed, 0, n, stream);
+}
+eIcicleError mbls_g1_msm_jacobian(const mbls_fr_t* scalars, const mbls_g1_affine_t* bases, int msm_size, const MSMConfig* config,
+                                   mbls_g1_projective_t* results) {
+    return msm_call<G>(scalars, bases, msm_size, config, results, MSM_JACOBIAN);
 }
 eIcicleError mbls_g1_sum_jacobian(const mbls_g1_projective_t* pts, int count, mbls_g1_projective_t* result,
                                   void* stream) {

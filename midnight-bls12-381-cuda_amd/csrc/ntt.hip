@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <memory>
 #include <mutex>
 
 #include "mbls_common.hpp"
@@ -42,15 +43,31 @@ static constexpr int NTT_PASS_STAGES = 8;
 static const uint64_t ROOT_2_32_MONT[4] = {0xb9b58d8c5f0e466aULL, 0x5b1b4c801819d7ecULL, 0x0af53ae352a31e64ULL,
                                            0x5bf3adda19e9b27bULL};
 
-struct Domain {
-    int order_log = 32;         // 2^order_log: order of the initialised root (size bound)
+// Twiddle tables of one domain build.  Callers take a shared_ptr snapshot under the lock and
+// enqueue their kernels with it; a table superseded by an extension or a release is freed only
+// when the last snapshot is dropped, after a device synchronisation, so no queued transform
+// ever reads freed memory (concurrent callers on rayon threads, SURVEY.md 8b "Threading").
+struct DomainTables {
     int max_log = 0;            // stage tables built for stages 1..max_log
     uint8_t* tw = nullptr;      // per-stage w_(2^s)^i tables (see header)
     uint8_t* tw_inv = nullptr;  // per-stage w_(2^s)^-i
+    ~DomainTables() {
+        if (tw || tw_inv) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(tw);
+            (void)hipFree(tw_inv);
+        }
+    }
+};
+
+struct Domain {
+    int order_log = 32;  // 2^order_log: order of the initialised root (size bound)
+    std::shared_ptr<DomainTables> tables;
 };
 
 static std::mutex g_domain_mu;
-static Domain g_domain;
+// never destroyed: freeing device memory during runtime teardown at exit is unsafe
+static Domain& g_domain = *new Domain();
 
 __device__ __forceinline__ uint32_t bitrev(uint32_t x, int bits) {
     return bits == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - bits));
@@ -301,43 +318,34 @@ static Fr to_dev(const uint64_t* h) {
     return r;
 }
 
+// (re)build the stage tables up to 2^max_log; caller holds g_domain_mu.  A superseded table
+// stays alive while any snapshot of it does (DomainTables)
 static eIcicleError build_domain(int max_log, hipStream_t st) {
-    if (g_domain.max_log >= max_log && g_domain.tw) return MBLS_SUCCESS;
-    if (g_domain.tw) {
-        MBLS_TRY(hipDeviceSynchronize());
-        (void)hipFree(g_domain.tw);
-        (void)hipFree(g_domain.tw_inv);
-        g_domain.tw = g_domain.tw_inv = nullptr;
-        g_domain.max_log = 0;
-    }
+    if (g_domain.tables && g_domain.tables->max_log >= max_log) return MBLS_SUCCESS;
     const int order = g_domain.order_log;
     if (max_log > order) return MBLS_INVALID_ARGUMENT;
     size_t count = ((size_t)1 << max_log) - 1;
     if (count == 0) count = 1;
-    uint8_t *tw = nullptr, *twi = nullptr;
-    MBLS_TRY(hipMalloc(&tw, 32 * count));
-    hipError_t e2 = hipMalloc(&twi, 32 * count);
-    if (e2 != hipSuccess) {
-        (void)hipFree(tw);
-        return map_hip_error(e2, "ntt twiddle alloc");
-    }
+    auto t = std::make_shared<DomainTables>();
+    MBLS_TRY(hipMalloc(&t->tw, 32 * count));
+    MBLS_TRY(hipMalloc(&t->tw_inv, 32 * count));
     uint64_t w[4], wi[4];
     canonical_omega(w, max_log);
     hfr_inv(wi, w);
     int blocks = (int)((count + 255) / 256);
-    hipLaunchKernelGGL(k_twiddles, dim3(blocks), dim3(256), 0, st, tw, to_dev(w), max_log, (uint32_t)count);
-    hipLaunchKernelGGL(k_twiddles, dim3(blocks), dim3(256), 0, st, twi, to_dev(wi), max_log, (uint32_t)count);
+    hipLaunchKernelGGL(k_twiddles, dim3(blocks), dim3(256), 0, st, t->tw, to_dev(w), max_log, (uint32_t)count);
+    hipLaunchKernelGGL(k_twiddles, dim3(blocks), dim3(256), 0, st, t->tw_inv, to_dev(wi), max_log, (uint32_t)count);
     MBLS_TRY(hipGetLastError());
     MBLS_TRY(hipStreamSynchronize(st));
-    g_domain.max_log = max_log;
-    g_domain.tw = tw;
-    g_domain.tw_inv = twi;
+    t->max_log = max_log;
+    g_domain.tables = std::move(t);
     return MBLS_SUCCESS;
 }
 
 // enqueue forward/inverse NTT of `batch` polynomials of 2^log_n on device buffers
-eIcicleError ntt_device(uint8_t* out, const uint8_t* in, int log_n, bool inverse, int batch, hipStream_t st) {
-    const Domain& D = g_domain;
+// (D: the caller's snapshot of the domain tables, kept alive across the enqueue)
+eIcicleError ntt_device(uint8_t* out, const uint8_t* in, int log_n, bool inverse, int batch, const DomainTables& D,
+                        hipStream_t st) {
     if (!D.tw || log_n > D.max_log) return MBLS_INVALID_ARGUMENT;
     const size_t n = (size_t)1 << log_n;
     const uint8_t* tw = inverse ? D.tw_inv : D.tw;
@@ -416,14 +424,14 @@ eIcicleError ntt_init_domain(const mbls_fr_t* root, const NTTInitDomainConfig* c
 }
 
 eIcicleError ntt_release_domain() {
-    std::lock_guard<std::mutex> lk(g_domain_mu);
-    if (g_domain.tw) {
-        MBLS_TRY(hipDeviceSynchronize());
-        (void)hipFree(g_domain.tw);
-        (void)hipFree(g_domain.tw_inv);
+    std::shared_ptr<DomainTables> old;
+    {
+        std::lock_guard<std::mutex> lk(g_domain_mu);
+        old = std::move(g_domain.tables);
+        g_domain.tables.reset();
+        g_domain.order_log = 32;
     }
-    g_domain = Domain{};
-    return MBLS_SUCCESS;
+    return MBLS_SUCCESS;  // `old` frees the tables here unless a transform still holds them
 }
 
 // coset scaling x_i *= g^(+-i) within each polynomial (device, in place)
@@ -485,16 +493,18 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
     const bool cols = cfg->columns_batch;
     int batch = cfg->batch_size > 0 ? cfg->batch_size : 1;
     hipStream_t st = static_cast<hipStream_t>(cfg->stream);
+    std::shared_ptr<DomainTables> tables;  // snapshot: valid for the whole enqueue below
     {
         std::lock_guard<std::mutex> lk(g_domain_mu);
         if (log_n > g_domain.order_log) return MBLS_INVALID_ARGUMENT;  // beyond the initialised root
-        if (!g_domain.tw || g_domain.max_log < log_n) {
+        if (!g_domain.tables || g_domain.tables->max_log < log_n) {
             // lazily extend the stage tables (init_domain builds up to 2^22)
             int want = log_n < 20 ? 20 : log_n;
             if (want > g_domain.order_log) want = g_domain.order_log;
             eIcicleError er = build_domain(want, st);
             if (er != MBLS_SUCCESS) return er;
         }
+        tables = g_domain.tables;
     }
     const size_t bytes = (size_t)size * 32 * (size_t)batch;
     const size_t total = (size_t)size * batch;
@@ -548,7 +558,7 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
         }
         win = t;
     }
-    er = ntt_device(wout, win, log_n, inverse, batch, st);
+    er = ntt_device(wout, win, log_n, inverse, batch, *tables, st);
     if (er != MBLS_SUCCESS) return er;
     if (coset && inverse) {
         uint64_t gi[4];
@@ -596,7 +606,7 @@ eIcicleError bls12_381_field_ntt_release_domain_cuda(void) { return ntt_release_
 eIcicleError bls12_381_ntt_get_rou_from_domain(uint64_t logn, mbls_fr_t* rou) {
     if (!rou) return MBLS_INVALID_POINTER;
     std::lock_guard<std::mutex> lk(g_domain_mu);
-    if (!g_domain.tw || logn > (uint64_t)g_domain.order_log) return MBLS_INVALID_ARGUMENT;
+    if (!g_domain.tables || logn > (uint64_t)g_domain.order_log) return MBLS_INVALID_ARGUMENT;
     canonical_omega(rou->limbs, (int)logn);
     return MBLS_SUCCESS;
 }

@@ -316,6 +316,54 @@ def signed_digits(s: int, c: int, num_windows: int):
     return out, carry
 
 
+def precompute_shift(factor: int) -> int:
+    """bits between consecutive multiples of a precomputed table [P, 2^s P, ...] (depends on
+    the factor only; msm_common.hip precompute_shift)"""
+    return -(-256 // factor) if factor > 1 else 0
+
+
+def block_windows(c: int, factor: int):
+    """(bit position, width) of every window of the precomputed-bases recoding
+    (msm_common.hip window_span): factor blocks of s bits, ceil(s / c) windows per block,
+    the last window of a block narrower when c does not divide s."""
+    s = precompute_shift(factor)
+    wg = -(-s // c)
+    return [(s * f + c * l, min(c, s - c * l)) for f in range(factor) for l in range(wg)], wg
+
+
+def signed_digits_blocks(x: int, c: int, factor: int):
+    """signed digits over block_windows: the carry runs through all windows in order, a window
+    narrower than c never carries (value + carry <= 2^(c-1)).  Returns (digits, final_carry)."""
+    half = 1 << (c - 1)
+    carry = 0
+    out = []
+    for pos, wid in block_windows(c, factor)[0]:
+        v = ((x >> pos) & ((1 << wid) - 1)) + carry
+        carry = 0
+        if v > half:
+            v -= 1 << c
+            carry = 1
+        out.append(v)
+    return out, carry
+
+
+def msm_precomputed(scalars, points, factor: int, c: int, group: str = "g1"):
+    """sum s_i P_i evaluated the way the precomputed-bases MSM does: table entry (i, f) =
+    2^(s f) P_i, digit (f, l) weighted 2^(c l) (small cases only)"""
+    mul, add = (g1_mul, g1_add) if group == "g1" else (g2_mul, g2_add)
+    s = precompute_shift(factor)
+    wins, wg = block_windows(c, factor)
+    acc = None
+    for k, pt in zip(scalars, points):
+        d, carry = signed_digits_blocks(k, c, factor)
+        assert carry == 0
+        for j, v in enumerate(d):
+            f, l = divmod(j, wg)
+            if v:
+                acc = add(acc, mul(v % R, mul(1 << (s * f + c * l), pt)))
+    return acc
+
+
 # --------------------------------------------------------------------------------------
 # GLV split used by the G1 MSM kernel (k_digits_glv).  Not a reference algorithm: the
 # reference ships GLV constants only behind an experimental flag, off the MSM path

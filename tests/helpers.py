@@ -118,6 +118,9 @@ def oracle():
         getattr(lib, nm).argtypes = [P, P, P, sz, ctypes.c_int]
         getattr(lib, nm).restype = ctypes.c_int
     lib.orc_gen_scalars.argtypes = [P, ctypes.c_uint64, sz]
+    lib.orc_set_threads.argtypes = [ctypes.c_int]
+    lib.orc_set_threads.restype = None
+    lib.orc_max_threads.restype = ctypes.c_int
     for nm in ("orc_gen_g1_bases", "orc_gen_g2_bases"):
         getattr(lib, nm).argtypes = [P, ctypes.c_uint64, sz, ctypes.c_int]
     _ORACLE = lib

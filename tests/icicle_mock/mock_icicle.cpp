@@ -114,10 +114,22 @@ static F sym(const char* name) {
 
 static int run_gpu(const char* dev_type) {
     DeviceAPI* api = g_dev().at(dev_type).get();
-    Device dev{dev_type, 0};
-    CHECK(api->set_device(dev) == eIcicleError::SUCCESS, "set_device");
+    // ICICLE's Device is {char type[32]; int id} (include/icicle/device.h:55-57): build it the
+    // way ICICLE's constructor does, so a backend reading `id` at the wrong offset is caught
+    auto make_dev = [](const char* type, int id) { return icicle::make_device(type, id); };
+    Device dev = make_dev(dev_type, 0);
     int count = 0;
     CHECK(api->get_device_count(count) == eIcicleError::SUCCESS && count >= 1, "get_device_count");
+    // an id past the last device must be rejected, not silently mapped to device 0
+    CHECK(api->set_device(make_dev(dev_type, count)) == eIcicleError::INVALID_DEVICE, "set_device(id = count) rejected");
+    CHECK(api->set_device(make_dev(dev_type, -1)) == eIcicleError::INVALID_DEVICE, "set_device(id = -1) rejected");
+    CHECK(api->set_device(dev) == eIcicleError::SUCCESS, "set_device");
+    {  // HostToHost (device_api.h:44) is a host memcpy, not a device-to-device copy
+        uint8_t src[64], dst[64];
+        for (int i = 0; i < 64; ++i) src[i] = (uint8_t)(3 * i + 1), dst[i] = 0;
+        CHECK(api->copy(dst, src, 64, eCopyDirection::HostToHost) == eIcicleError::SUCCESS && memcmp(dst, src, 64) == 0,
+              "copy HostToHost");
+    }
     icicleStreamHandle st = nullptr;
     CHECK(api->create_stream(&st) == eIcicleError::SUCCESS && st, "create_stream");
 

@@ -365,10 +365,48 @@ def test_msm_precompute_factor(amd, gh):
     s_std, _, b_mont = _case_arrays(gh, case, "g1")
     n = s_std.shape[0]
     expect = H.pt_from_json(case["result"], "g1")
-    for c, factor in [(8, 2), (8, 4), (10, 26), (13, 5)]:
+    for c, factor in [(8, 2), (8, 4), (10, 26), (13, 5), (3, 64)]:
         pre = amd.precompute_bases("g1", b_mont, factor, n, c=c)
         r = amd.msm("g1", s_std, pre, c=c, precompute_factor=factor, n=n)
         assert gh.decode_icicle("g1", r[0]) == expect, (c, factor)
+
+
+@pytest.mark.parametrize("group", ["g1", "g2"])
+def test_msm_precompute_replays_rust_caller(amd, gh, group):
+    """core/msm.rs flag for flag: precompute_bases (:441-454: c = 0, bases Montgomery, factor
+    1..8) once over the whole base set, then msm_with_device_bases (:630-650): host scalars in
+    Montgomery form, the FULL precomputed buffer, are_bases_montgomery_form = !is_precomputed()
+    (false for a table), c = MIDNIGHT_MSM_WINDOW (0 = auto) and msm_size <= bases_size.  The
+    table's shift depends on the factor only, so every c / msm_size must give the oracle's sum."""
+    import torch
+    nb, n = (3000, 2500) if group == "g1" else (700, 600)
+    w = 12 if group == "g1" else 24
+    b = torch.zeros((nb, w), dtype=torch.int64, device="cuda")
+    amd.gen_bases(group, b, 0x5EED00C1)
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED00C2, montgomery=False)
+    sm = torch.zeros_like(s)
+    amd.gen_scalars(sm, 0x5EED00C2, montgomery=True)  # same stream, Montgomery form (host copy below)
+    torch.cuda.synchronize()
+    s_std, s_mont = amd.to_numpy_u64(s), np.ascontiguousarray(amd.to_numpy_u64(sm))
+    bn = amd.to_numpy_u64(b)
+    ref = H.oracle_msm(group, s_std, np.ascontiguousarray(bn[:n]))
+    dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
+    for factor in (1, 2, 3, 4, 8) if group == "g1" else (1, 4, 7):
+        table = torch.zeros((nb * factor, w), dtype=torch.int64, device="cuda")
+        amd.precompute_bases(group, b, factor, nb, c=0, out=table)  # core/msm.rs:451: cfg.c = 0
+        for c in (0, 11, 16):
+            r = amd.msm(group, s_mont, table, scalars_mont=True, points_mont=(factor == 1), c=c,
+                        precompute_factor=factor, n=n)
+            assert gh.decode_icicle(group, r[0]) == dec(ref), (factor, c)
+    # standard-form input to the precompute is converted (the output is always Montgomery)
+    pts_std = np.ascontiguousarray(bn.copy())
+    for k in range(pts_std.shape[0]):
+        pts_std[k] = [v for fq in range(w // 6) for v in pr.int_to_limbs(pr.fq_from_mont(pr.limbs_to_int(
+            [int(x) for x in bn[k, 6 * fq:6 * fq + 6]])), 6)]
+    table = amd.precompute_bases(group, pts_std, 2, nb, points_mont=False)
+    r = amd.msm(group, s_std, table, points_mont=False, precompute_factor=2, n=n)
+    assert gh.decode_icicle(group, r[0]) == dec(ref)
 
 
 def test_msm_batch(amd, gh):
@@ -476,12 +514,78 @@ def test_msm_psi_split_boundaries(amd, gh):
     assert gh.decode_icicle("g2", r[0]) == ref
 
 
-@pytest.mark.slow
-def test_msm_g1_2_24_bit_exact(amd, gh):
-    """north-star size: G1 MSM of 2^24 points (BASELINE config #4 total size, single GPU) equals
-    the oracle's multithreaded Pippenger bit-exactly (canonical affine)"""
+# ----------------------------------------------------------------------------- benchmarked workloads
+# bench.py's inputs exactly (seeds, sizes, entry points, flags), bit-exact against the oracle
+ORACLE_THREADS = 16  # the GPU box's CPU share
+
+
+def _oracle_std_scalars(seed, n, start=0):
+    s = np.zeros((start + n, 4), dtype=np.uint64)
+    H.oracle().orc_gen_scalars(H.ptr(s), seed, start + n)
+    return np.ascontiguousarray(s[start:])
+
+
+@pytest.mark.parametrize("group,seeds", [("g1", (0x5EED0003, 0x5EED0013)), ("g2", (0x5EED0005, 0x5EED0015))])
+def test_bench_msm_2_20_production_path(amd, gh, group, seeds):
+    """bench.py headline (G1) and config #5 (G2) MSM: 2^20 points, Montgomery scalars and bases
+    resident on the device, ICICLE entry ((x, y, 1) result on the device), async on a stream --
+    the call core/msm.rs:594-682 makes (core/traits/cpu_impl.rs:117-165 is the CPU semantics)"""
     import torch
-    n = 1 << 24
+    n = 1 << 20
+    w = 12 if group == "g1" else 24
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, seeds[0], montgomery=True)
+    b = torch.zeros((n, w), dtype=torch.int64, device="cuda")
+    amd.gen_bases(group, b, seeds[1])
+    out = torch.zeros((1, w * 3 // 2), dtype=torch.int64, device="cuda")
+    st = torch.cuda.Stream()
+    amd.msm(group, s, b, scalars_mont=True, out=out, stream=st, is_async=True, n=n)
+    st.synchronize()
+    got = gh.decode_icicle(group, amd.to_numpy_u64(out)[0])
+    ref = H.oracle_msm(group, _oracle_std_scalars(seeds[0], n), amd.to_numpy_u64(b), threads=ORACLE_THREADS)
+    dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
+    assert got == dec(ref)
+
+
+def test_bench_ntt_2_22_single_and_batch4(amd):
+    """bench.py NTT 2^22 (seed 0x5EED0025, forward, natural order) and the config #5 batch of 4 x
+    2^22 (the mix leg's inputs), each member vs the oracle's best_fft DFT (core/ntt.rs:1488-1603)"""
+    import torch
+    amd.ntt_init_domain()
+    log_n, B = 22, 4
+    n = 1 << log_n
+    x = torch.zeros((B * n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(x, 0x5EED0025, montgomery=True)
+    y1 = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.ntt(x[:n], out=y1)
+    yb = torch.zeros_like(x)
+    amd.ntt(x, out=yb, batch=B)
+    torch.cuda.synchronize()
+    xn = amd.to_numpy_u64(x)
+    ybn = amd.to_numpy_u64(yb)
+    for k in range(B):
+        ref = H.oracle_ntt(xn[k * n:(k + 1) * n], log_n, False, threads=ORACLE_THREADS)
+        if k == 0:
+            assert np.array_equal(amd.to_numpy_u64(y1), ref)
+        assert np.array_equal(ybn[k * n:(k + 1) * n], ref), k
+    # inverse of the batch returns the inputs exactly
+    z = torch.zeros_like(x)
+    amd.ntt(yb, inverse=True, out=z, batch=B)
+    torch.cuda.synchronize()
+    assert torch.equal(z, x)
+
+
+@pytest.mark.slow
+def test_msm_g1_2_24_single_and_sharded(amd, gh):
+    """north-star size (BASELINE config #4): G1 MSM of 2^24 points (scalars 0x5EED0004, bases
+    0x5EED0013) on one GPU through the ICICLE entry, and the bench's sharded sequence for 8
+    ranks -- each shard of 2^21 generated from its slice of the global streams, one Jacobian
+    partial per shard (mbls_g1_msm_jacobian), partials stacked as the all-gather would, summed
+    (mbls_g1_sum_jacobian) and normalised once (mbls_g1_jacobian_to_icicle) -- both equal to
+    the oracle's multithreaded Pippenger bit-exactly"""
+    import sharded_msm
+    import torch
+    n, world = 1 << 24, 8
     s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
     amd.gen_scalars(s, 0x5EED0004, montgomery=True)
     b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
@@ -489,9 +593,22 @@ def test_msm_g1_2_24_bit_exact(amd, gh):
     out = torch.zeros((1, 18), dtype=torch.int64, device="cuda")
     amd.msm("g1", s, b, scalars_mont=True, out=out)
     torch.cuda.synchronize()
-    got = gh.decode_icicle("g1", amd.to_numpy_u64(out)[0])
-    del s
-    s_std = np.zeros((n, 4), dtype=np.uint64)
-    H.oracle().orc_gen_scalars(H.ptr(s_std), 0x5EED0004, n)
-    ref = H.oracle_msm("g1", s_std, amd.to_numpy_u64(b), threads=16)
-    assert got == H.g1_from_affine_mont(ref)
+    single = gh.decode_icicle("g1", amd.to_numpy_u64(out)[0])
+    bn = amd.to_numpy_u64(b)
+    del s, b
+    parts = torch.zeros((world, 18), dtype=torch.int64, device="cuda")
+    for r in range(world):
+        lo, hi = sharded_msm.shard_range(n, world, r)
+        ss = torch.zeros((hi - lo, 4), dtype=torch.int64, device="cuda")
+        amd.gen_scalars(ss, 0x5EED0004, montgomery=True, start=lo)
+        bs = torch.zeros((hi - lo, 12), dtype=torch.int64, device="cuda")
+        amd.gen_bases("g1", bs, 0x5EED0013, start=lo)
+        amd.msm("g1", ss, bs, icicle="jacobian", scalars_mont=True, out=parts[r:r + 1], n=hi - lo)
+    tot = torch.zeros((1, 18), dtype=torch.int64, device="cuda")
+    amd.sum_jacobian("g1", parts, tot)
+    amd.jacobian_to_icicle("g1", tot)
+    torch.cuda.synchronize()
+    sharded = gh.decode_icicle("g1", amd.to_numpy_u64(tot)[0])
+    ref = H.g1_from_affine_mont(H.oracle_msm("g1", _oracle_std_scalars(0x5EED0004, n), bn, threads=ORACLE_THREADS))
+    assert single == ref
+    assert sharded == ref

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Fixed workload for PMC passes (tools/gpu_pmc.sh): `--reps` G1 MSMs of 2^20 (bench.py's
-inputs and call) and `--reps` forward Fr NTTs of 2^22, nothing else, so per-kernel counter
-averages are per launch of exactly the benchmarked configurations."""
+headline inputs and call: ICICLE entry, Montgomery scalars, device bases and result) and
+`--reps` forward Fr NTTs of 2^22, nothing else, so per-kernel counter averages are per launch
+of exactly the benchmarked configurations."""
 import argparse
 import os
 import sys
@@ -26,7 +27,7 @@ def main():
     amd.gen_bases("g1", b, 0x5EED0013)
     out = torch.zeros((1, 18), dtype=torch.int64, device=dev)
     for _ in range(a.reps):
-        amd.msm("g1", s, b, icicle=False, scalars_mont=True, out=out, is_async=True, n=n)
+        amd.msm("g1", s, b, icicle=True, scalars_mont=True, out=out, is_async=True, n=n)
     torch.cuda.synchronize()
     amd.ntt_init_domain()
     x = torch.zeros((1 << a.ntt_log, 4), dtype=torch.int64, device=dev)
