@@ -538,6 +538,9 @@ def test_bench_msm_2_20_production_path(amd, gh, group, seeds):
     b = torch.zeros((n, w), dtype=torch.int64, device="cuda")
     amd.gen_bases(group, b, seeds[1])
     out = torch.zeros((1, w * 3 // 2), dtype=torch.int64, device="cuda")
+    # torch's side streams are non-blocking: they do not order behind the null stream the
+    # generators ran on
+    torch.cuda.synchronize()
     st = torch.cuda.Stream()
     amd.msm(group, s, b, scalars_mont=True, out=out, stream=st, is_async=True, n=n)
     st.synchronize()
