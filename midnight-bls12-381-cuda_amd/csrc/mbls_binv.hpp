@@ -1,0 +1,221 @@
+// mbls_binv.hpp -- modular inversion by the batched binary GCD (Pornin, "Optimized Binary GCD
+// for Modular Inversion", IACR ePrint 2020/972, algorithm 2; variable-time form).
+//
+// The hot-path products are quarter-rate v_mad_u64_u32 chains; a Fermat inversion a^(m-2) is
+// ~570 of them in series (0.29 ms on one row-sliced wave for the one (x, y, 1) normalisation of
+// an MSM result).  The binary GCD needs no products in its inner loop: 31 steps run on 64-bit
+// approximations of (a, b) (exact low 31 bits, top 33 bits), recording the update matrix
+// (f0 g0; f1 g1); the 12-word values are then updated once per 31 steps with word-by-word
+// small-factor products.  ~25 outer steps for a 381-bit modulus.
+//
+// Invariants (integers a, b >= 0; u, v mod m; y the input): a = u*y, b = v*y (mod m).  Start
+// a = y, b = m, u = 1, v = 0; each outer step maps (a, b) -> ((f0 a + g0 b) / 2^31, (f1 a + g1 b)
+// / 2^31) and (u, v) the same way mod m (exact division for a, b; Montgomery division by 2^31
+// for u, v).  The loop ends at a = 0 with b = gcd(y, m) = 1 and v = 1/y.
+//
+// Portable C++ (host-testable: tests/test_oracle.py builds tests/binv_host.cpp against it).
+#pragma once
+#include <stdint.h>
+
+#ifndef MBLS_HD
+#if defined(__HIPCC__)
+#define MBLS_HD __host__ __device__ __forceinline__
+#else
+#define MBLS_HD inline
+#endif
+#endif
+
+namespace mbls {
+namespace binv {
+
+template <int N>
+MBLS_HD bool is_zero(const uint32_t (&a)[N]) {
+    uint32_t t = 0;
+    for (int i = 0; i < N; ++i) t |= a[i];
+    return t == 0;
+}
+
+template <int N>
+MBLS_HD int bitlen(const uint32_t (&a)[N]) {
+    for (int i = N - 1; i >= 0; --i)
+        if (a[i]) return 32 * i + 32 - __builtin_clz(a[i]);
+    return 0;
+}
+
+// (a >> pos) & (2^33 - 1) for 0 <= pos, when a < 2^(pos + 33)
+template <int N>
+MBLS_HD uint64_t top33(const uint32_t (&a)[N], int pos) {
+    const int wi = pos >> 5, sh = pos & 31;
+    uint32_t w0 = 0, w1 = 0, w2 = 0;
+    for (int i = 0; i < N; ++i) {  // selects, not dynamic register indexing
+        w0 = i == wi ? a[i] : w0;
+        w1 = i == wi + 1 ? a[i] : w1;
+        w2 = i == wi + 2 ? a[i] : w2;
+    }
+    uint64_t x = ((uint64_t)w1 << 32) | w0;
+    x >>= sh;
+    if (sh) x |= (uint64_t)w2 << (64 - sh);
+    return x & ((1ull << 33) - 1);
+}
+
+// r (N+1 words) = a * k
+template <int N>
+MBLS_HD void mul_small(uint32_t (&r)[N + 1], const uint32_t (&a)[N], uint32_t k) {
+    uint64_t c = 0;
+    for (int i = 0; i < N; ++i) {
+        c += (uint64_t)a[i] * k;
+        r[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    r[N] = (uint32_t)c;
+}
+
+// S = s_p * P + s_q * Q as sign + magnitude (N+1 words); returns true if negative
+template <int M>
+MBLS_HD bool signed_sum(uint32_t (&S)[M], const uint32_t (&P)[M], bool np, const uint32_t (&Q)[M], bool nq) {
+    if (np == nq) {
+        uint64_t c = 0;
+        for (int i = 0; i < M; ++i) {
+            c += (uint64_t)P[i] + Q[i];
+            S[i] = (uint32_t)c;
+            c >>= 32;
+        }
+        return np;
+    }
+    int64_t br = 0;
+    for (int i = 0; i < M; ++i) {
+        int64_t d = (int64_t)P[i] - Q[i] + br;
+        S[i] = (uint32_t)d;
+        br = d >> 32;  // 0 or -1
+    }
+    if (br) {  // P < Q: magnitude Q - P, sign of Q
+        uint64_t c = 1;
+        for (int i = 0; i < M; ++i) {
+            c += (uint32_t)~S[i];
+            S[i] = (uint32_t)c;
+            c >>= 32;
+        }
+        return nq;
+    }
+    return np;
+}
+
+// r = |f a + g b| / 2^31 (exact); returns true if f a + g b < 0.  |f|, |g| <= 2^31.
+template <int N>
+MBLS_HD bool lincomb_shift(uint32_t (&r)[N], const uint32_t (&a)[N], const uint32_t (&b)[N], int64_t f, int64_t g) {
+    uint32_t P[N + 1], Q[N + 1], S[N + 1];
+    mul_small<N>(P, a, (uint32_t)(f < 0 ? -f : f));
+    mul_small<N>(Q, b, (uint32_t)(g < 0 ? -g : g));
+    const bool neg = signed_sum<N + 1>(S, P, f < 0, Q, g < 0);
+    for (int i = 0; i < N; ++i) r[i] = (S[i] >> 31) | (S[i + 1] << 1);
+    return neg && !is_zero<N>(r);
+}
+
+// r = (f u + g v) / 2^31 mod m, u, v in [0, m); result in [0, m).  |f|, |g| <= 2^31.
+template <int N>
+MBLS_HD void lincomb_mod(uint32_t (&r)[N], const uint32_t (&u)[N], const uint32_t (&v)[N], int64_t f, int64_t g,
+                         const uint32_t (&m)[N], uint32_t ninv) {
+    uint32_t P[N + 1], Q[N + 1], S[N + 1];
+    mul_small<N>(P, u, (uint32_t)(f < 0 ? -f : f));
+    mul_small<N>(Q, v, (uint32_t)(g < 0 ? -g : g));
+    const bool neg = signed_sum<N + 1>(S, P, f < 0, Q, g < 0);
+    if (neg) {  // |S| < 2^32 m: S <- 2^32 m - |S|, in (0, 2^32 m]
+        int64_t br = 0;
+        for (int i = 0; i <= N; ++i) {
+            const uint32_t mw = i == 0 ? 0u : m[i - 1];
+            int64_t d = (int64_t)mw - S[i] + br;
+            S[i] = (uint32_t)d;
+            br = d >> 32;
+        }
+    }
+    // S + k m = 0 (mod 2^31), k = S * (-1/m) mod 2^31; S + k m < 3 * 2^31 m < 2^(32(N+1))
+    const uint32_t k = (S[0] * ninv) & 0x7fffffffu;
+    uint64_t c = 0;
+    for (int i = 0; i <= N; ++i) {
+        c += (uint64_t)S[i] + (i < N ? (uint64_t)m[i] * k : 0ull);
+        S[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    // (S + k m) / 2^31 < 3m: N + 1 words (3r > 2^256 for the 255-bit Fr modulus)
+    uint32_t t[N + 1];
+    for (int i = 0; i < N; ++i) t[i] = (S[i] >> 31) | (S[i + 1] << 1);
+    t[N] = S[N] >> 31;
+    for (int q = 0; q < 2; ++q) {
+        uint32_t d[N + 1];
+        int64_t br = 0;
+        for (int i = 0; i <= N; ++i) {
+            int64_t x = (int64_t)t[i] - (i < N ? m[i] : 0u) + br;
+            d[i] = (uint32_t)x;
+            br = x >> 32;
+        }
+        if (!br)
+            for (int i = 0; i <= N; ++i) t[i] = d[i];
+    }
+    for (int i = 0; i < N; ++i) r[i] = t[i];
+}
+
+// out = 1 / y mod m (plain integers, y in [1, m), m odd, gcd(y, m) = 1).  Returns the number of
+// outer steps (<= 2 * bitlen(m) / 31 + 2 for valid input; capped so a bad input still ends).
+template <int N>
+MBLS_HD int inverse(uint32_t (&out)[N], const uint32_t (&y)[N], const uint32_t (&m)[N], uint32_t ninv) {
+    uint32_t a[N], b[N], u[N], v[N];
+    for (int i = 0; i < N; ++i) {
+        a[i] = y[i];
+        b[i] = m[i];
+        u[i] = i == 0 ? 1u : 0u;
+        v[i] = 0;
+    }
+    int steps = 0;
+    const int cap = (64 * N) / 31 + 8;
+    while (!is_zero<N>(a) && steps < cap) {
+        ++steps;
+        const int la = bitlen<N>(a), lb = bitlen<N>(b);
+        const int n = la > lb ? (la > 64 ? la : 64) : (lb > 64 ? lb : 64);
+        uint64_t xa = (a[0] & 0x7fffffffu) | (top33<N>(a, n - 33) << 31);
+        uint64_t xb = (b[0] & 0x7fffffffu) | (top33<N>(b, n - 33) << 31);
+        int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+        for (int j = 0; j < 31; ++j) {
+            if (xa & 1) {
+                if (xa < xb) {
+                    const uint64_t t = xa;
+                    xa = xb;
+                    xb = t;
+                    int64_t s = f0;
+                    f0 = f1;
+                    f1 = s;
+                    s = g0;
+                    g0 = g1;
+                    g1 = s;
+                }
+                xa -= xb;
+                f0 -= f1;
+                g0 -= g1;
+            }
+            xa >>= 1;
+            f1 <<= 1;
+            g1 <<= 1;
+        }
+        uint32_t na[N], nb[N], nu[N], nv[N];
+        if (lincomb_shift<N>(na, a, b, f0, g0)) {
+            f0 = -f0;
+            g0 = -g0;
+        }
+        if (lincomb_shift<N>(nb, a, b, f1, g1)) {
+            f1 = -f1;
+            g1 = -g1;
+        }
+        lincomb_mod<N>(nu, u, v, f0, g0, m, ninv);
+        lincomb_mod<N>(nv, u, v, f1, g1, m, ninv);
+        for (int i = 0; i < N; ++i) {
+            a[i] = na[i];
+            b[i] = nb[i];
+            u[i] = nu[i];
+            v[i] = nv[i];
+        }
+    }
+    for (int i = 0; i < N; ++i) out[i] = v[i];
+    return steps;
+}
+
+}  // namespace binv
+}  // namespace mbls

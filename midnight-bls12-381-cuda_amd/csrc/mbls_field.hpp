@@ -182,6 +182,7 @@ MBLS_DEV Fp<C> mul_cios(const Fp<C>& a, const Fp<C>& b) {
 
 }  // namespace mbls
 #include "mbls_fips.hpp"
+#include "mbls_binv.hpp"
 namespace mbls {
 
 template <class C>
@@ -237,9 +238,10 @@ MBLS_DEV Fp<C> pow_words(const Fp<C>& a, const uint32_t (&e)[EW]) {
     return acc;
 }
 
-// Fermat inversion a^(m-2); 0 -> 0 (reference field.cuh:750-900 semantics)
+// Fermat inversion a^(m-2); 0 -> 0 (reference field.cuh:750-900 semantics).  Kept for the
+// row-sliced types and as the cross-check of inv() below.
 template <class C>
-MBLS_DEV Fp<C> inv(const Fp<C>& a) {
+MBLS_DEV Fp<C> inv_fermat(const Fp<C>& a) {
     uint32_t e[C::N];
 #pragma unroll
     for (int i = 0; i < C::N; ++i) e[i] = C::MOD[i];
@@ -252,6 +254,24 @@ MBLS_DEV Fp<C> inv(const Fp<C>& a) {
         e[i] = d;
     }
     return pow_words<C, C::N>(a, e);
+}
+
+// Inversion by the batched binary GCD (mbls_binv.hpp; variable time -- this path is not
+// constant-time): full-rate word operations plus ~100 small-factor word products
+// per 31 steps, where the Fermat chain above is ~570 serial Montgomery products.  The input's
+// Montgomery limbs are inverted as an integer, (aR)^-1, then one product with R^3 (= R2 * R2 in
+// Montgomery form) gives a^-1 R.  0 -> 0 (field.cuh:750-900 semantics).
+template <class C>
+MBLS_DEV Fp<C> inv(const Fp<C>& a) {
+    constexpr int N = C::N;
+    if (a.is_zero()) return a;
+    uint32_t m[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) m[i] = C::MOD[i];
+    Fp<C> x;
+    binv::inverse<N>(x.v, a.v, m, C::NINV);
+    const Fp<C> r2 = Fp<C>::r2();
+    return x * (r2 * r2);
 }
 
 // ------------------------------------------------------------------------------------

@@ -56,6 +56,7 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     p.Wg = Wg;
     p.B = 1u << (c - 1);
     p.TB = (uint32_t)Wg * p.B;
+    p.chunk = CHUNK;  // msm_call replaces it with accumulate_chunk<F>(contributions)
     p.pts = (size_t)n * (p.split > 1 ? p.split : F);  // point indices (P_i, then the images)
     p.contributions = (size_t)n * W * p.split;
     if (p.pts >= (1u << 31)) return MBLS_INVALID_ARGUMENT;
@@ -991,18 +992,22 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
     return MBLS_SUCCESS;
 }
 
-// Chunks are 16-ALIGNED in the sorted array (chunk t = positions [16t, 16t + 16)), so every
-// accumulation thread does exactly 16 additions; a chunk crossing bucket boundaries yields one
+// Chunks are L-ALIGNED in the sorted array (chunk t = positions [L t, L t + L)), so every
+// accumulation thread does exactly L additions; a chunk crossing bucket boundaries yields one
 // partial ("segment") per bucket it touches.  Segments of bucket b: the aligned chunks that
 // overlap [off_b, off_b + cnt_b).  nchunks[m] receives the maximum (heavy-bucket passes).
 __global__ void k_chunk_counts(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offsets,
-                               uint32_t* __restrict__ nchunks, uint32_t m) {
+                               uint32_t* __restrict__ nchunks, uint32_t m, uint32_t L, uint32_t* __restrict__ binhist) {
+    __shared__ uint32_t hist[ORDER_BINS];
+    if (threadIdx.x < ORDER_BINS) hist[threadIdx.x] = 0;
+    __syncthreads();
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t c = 0;
     if (b < m) {
         const uint32_t cnt = counts[b], o = offsets[b];
-        c = cnt ? (o + cnt - 1) / CHUNK - o / CHUNK + 1 : 0u;
+        c = cnt ? (o + cnt - 1) / L - o / L + 1 : 0u;
         nchunks[b] = c;
+        if (c <= SMALL_MAX) atomicAdd(&hist[c], 1u);
     }
     // block max, then at most one atomic per block and only when it raises the running max
     // (4096 same-address atomics cost 46 us at 2^20; the filtered read is monotone-safe)
@@ -1014,12 +1019,39 @@ __global__ void k_chunk_counts(const uint32_t* __restrict__ counts, const uint32
         c = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
         if (c > 1 && c > __atomic_load_n(&nchunks[m], __ATOMIC_RELAXED)) atomicMax(&nchunks[m], c);
     }
+    // per-block histogram of the light buckets' chunk counts, bin-major (k_bucket_order)
+    if (threadIdx.x < ORDER_BINS) binhist[threadIdx.x * gridDim.x + blockIdx.x] = hist[threadIdx.x];
+}
+
+// perm = the light buckets (<= SMALL_MAX chunks) grouped by chunk count, so the waves of
+// k_bucket_small run uniform trip counts (bucket order alone gave ~4 +- 1.5 chunks per lane and
+// a wave ran its maximum).  binbase = exclusive scan of k_chunk_counts' bin-major histograms.
+__global__ void k_bucket_order(const uint32_t* __restrict__ nchunks, uint32_t m, const uint32_t* __restrict__ binbase,
+                               uint32_t* __restrict__ perm) {
+    __shared__ uint32_t cur[ORDER_BINS];
+    if (threadIdx.x < ORDER_BINS) cur[threadIdx.x] = binbase[threadIdx.x * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= m) return;
+    const uint32_t c = nchunks[b];
+    if (c <= SMALL_MAX) perm[atomicAdd(&cur[c], 1u)] = b;
 }
 
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
-                                 hipStream_t st) {
+                                 uint32_t L, uint32_t* binhist, hipStream_t st) {
     MBLS_TRY(hipMemsetAsync(nchunks + m, 0, 4, st));
-    hipLaunchKernelGGL(k_chunk_counts, dim3((m + 255) / 256), dim3(256), 0, st, counts, offsets, nchunks, m);
+    hipLaunchKernelGGL(k_chunk_counts, dim3((m + 255) / 256), dim3(256), 0, st, counts, offsets, nchunks, m, L, binhist);
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
+}
+
+uint32_t order_words(uint32_t m) { return ORDER_BINS * ((m + 255) / 256); }
+
+eIcicleError launch_bucket_order(const uint32_t* nchunks, uint32_t m, const uint32_t* binhist, uint32_t* binbase,
+                                 uint32_t* tmp, uint32_t* perm, hipStream_t st) {
+    eIcicleError er = scan_exclusive(binhist, binbase, order_words(m), tmp, st);
+    if (er != MBLS_SUCCESS) return er;
+    hipLaunchKernelGGL(k_bucket_order, dim3((m + 255) / 256), dim3(256), 0, st, nchunks, m, binbase, perm);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }
@@ -1045,19 +1077,19 @@ eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const ui
     return MBLS_SUCCESS;
 }
 
-// owner[segment] = bucket; first[t] = the bucket holding position 16t (the start of chunk t)
+// owner[segment] = bucket; first[t] = the bucket holding position L t (the start of chunk t)
 __global__ void k_chunk_owner(const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ offsets, uint32_t m,
-                              uint32_t* __restrict__ owner, uint32_t* __restrict__ first) {
+                              uint32_t L, uint32_t* __restrict__ owner, uint32_t* __restrict__ first) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
     for (uint32_t k = chunk_off[b]; k < chunk_off[b + 1]; ++k) owner[k] = b;
     const uint32_t o = offsets[b], e = offsets[b + 1];
-    for (uint32_t t = (o + CHUNK - 1) / CHUNK; t * CHUNK < e; ++t) first[t] = b;
+    for (uint32_t t = (o + L - 1) / L; t * L < e; ++t) first[t] = b;
 }
 
-eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offsets, uint32_t m, uint32_t* owner,
-                                uint32_t* first, hipStream_t st) {
-    hipLaunchKernelGGL(k_chunk_owner, dim3((m + 255) / 256), dim3(256), 0, st, chunk_off, offsets, m, owner, first);
+eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offsets, uint32_t m, uint32_t L,
+                                uint32_t* owner, uint32_t* first, hipStream_t st) {
+    hipLaunchKernelGGL(k_chunk_owner, dim3((m + 255) / 256), dim3(256), 0, st, chunk_off, offsets, m, L, owner, first);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }

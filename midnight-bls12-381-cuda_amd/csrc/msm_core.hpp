@@ -27,6 +27,7 @@
 // the W windows into Wg = ceil(W/F) groups so the final fold shrinks to (Wg-1)*c doublings.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -57,12 +58,15 @@ static constexpr int SCAN_BLOCK = 1024;
 static constexpr int MAX_LEVELS = 16;
 
 static constexpr int MAX_PRECOMPUTE = 64;
+static constexpr int SMALL_MAX = 16;  // buckets of <= SMALL_MAX chunks: one thread (k_bucket_small)
+static constexpr int ORDER_BINS = SMALL_MAX + 1;  // k_bucket_order bins: chunk counts 0..SMALL_MAX
 
 struct MsmPlan {
     int c, W, Wg, F;
     int sF;                     // precomputed-table block shift in bits (0: F == 1), see window_span
     int split;                  // endomorphism split: 1 none, 2 G1 GLV (phi), 4 G2 psi
     uint32_t B, TB;
+    uint32_t chunk;             // contributions per accumulation thread (accumulate_chunk)
     size_t pts;                 // distinct point indices (n, n*F, or split*n)
     size_t contributions;
     int levels;                 // bucket-reduction levels
@@ -88,11 +92,14 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
 size_t digits_src_bytes(uint32_t n, int split);
 eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint32_t* tmp, hipStream_t st);
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
-                                 hipStream_t st);
+                                 uint32_t L, uint32_t* binhist, hipStream_t st);
+eIcicleError launch_bucket_order(const uint32_t* nchunks, uint32_t m, const uint32_t* binhist, uint32_t* binbase,
+                                 uint32_t* tmp, uint32_t* perm, hipStream_t st);
+uint32_t order_words(uint32_t m);
 eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const uint32_t* ranks, size_t total,
                             const uint32_t* offsets, uint32_t* sorted, hipStream_t st);
-eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offsets, uint32_t m, uint32_t* owner,
-                                uint32_t* first, hipStream_t st);
+eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offsets, uint32_t m, uint32_t L,
+                                uint32_t* owner, uint32_t* first, hipStream_t st);
 eIcicleError launch_scalars_from_mont(uint8_t* s, size_t n, hipStream_t st);
 eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
 eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
@@ -116,24 +123,26 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
                               uint32_t* offsets, uint32_t* sorted, hipStream_t st);
 
 // ------------------------------------------------------------------------------------
-// 4. accumulation: thread t sums the 16 contributions at sorted positions [16t, 16t + 16),
+// 4. accumulation: thread t sums the L contributions at sorted positions [L t, L t + L),
 //    one partial per bucket segment it touches (see k_chunk_counts): no idle lanes on the
-//    short last chunk of each bucket.
+//    short last chunk of each bucket.  L (accumulate_chunk) spreads the contributions evenly
+//    over ONE round of resident waves: no partly filled last round, and ~1.3 partials per
+//    bucket at 2^20 instead of ~4 with 16-point chunks.
 // ------------------------------------------------------------------------------------
 template <class F, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ chunk_off,
                                                     const uint32_t* __restrict__ first, uint32_t TB,
                                                     const uint8_t* __restrict__ bases, const uint8_t* __restrict__ phi,
-                                                    uint32_t nsplit, uint8_t* __restrict__ partials) {
+                                                    uint32_t nsplit, uint32_t chunk, uint8_t* __restrict__ partials) {
     using L = typename LaneOf<F>::type;
     const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
     const uint32_t total = offsets[TB];
-    const uint32_t beg = t * CHUNK;
+    const uint32_t beg = t * chunk;
     if (beg >= total) return;
-    const uint32_t end = min(beg + CHUNK, total);
+    const uint32_t end = min(beg + chunk, total);
     uint32_t b = first[t];
-    uint32_t seg = chunk_off[b] + (t - offsets[b] / CHUNK);
+    uint32_t seg = chunk_off[b] + (t - offsets[b] / chunk);
     uint32_t bend = offsets[b + 1];
     Jacobian<L> acc = Jacobian<L>::inf();
     // endomorphism split: indices >= nsplit address the image table (phi(P) / psi^j(P))
@@ -195,7 +204,6 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
 //    (maxc = max chunks per bucket, computed on device).
 // ------------------------------------------------------------------------------------
 static constexpr int TREE_FANIN = 8;
-static constexpr int SMALL_MAX = 16;  // buckets of <= SMALL_MAX chunks: one thread (k_bucket_small)
 
 template <class F>
 __global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict__ chunk_off,
@@ -223,18 +231,21 @@ __global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict_
     }
 }
 
-// common case: one thread per bucket sums its <= SMALL_MAX chunk partials
+// common case: one thread per light bucket (<= SMALL_MAX chunks) sums its chunk partials;
+// thread t takes perm[t] (k_bucket_order: buckets grouped by chunk count, so a wave's lanes run
+// the same number of additions).  nlight = the order scan's total.
 template <class F>
 #ifndef MBLS_BS_MINW
 #define MBLS_BS_MINW 1
 #endif
-__global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32_t* __restrict__ chunk_off, uint32_t m,
+__global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32_t* __restrict__ chunk_off,
+                                                      const uint32_t* __restrict__ perm, const uint32_t* __restrict__ nlight,
                                                       const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
     using L = typename LaneOf<F>::type;
-    uint32_t b = (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
-    if (b >= m) return;
+    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
+    if (t >= *nlight) return;
+    const uint32_t b = perm[t];
     const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
-    if (k1 - k0 > SMALL_MAX) return;  // heavy: tree passes + k_bucket_gather
     Jacobian<L> acc = Jacobian<L>::inf();
     if (k1 > k0) acc = load_jac<L>(partials, k0);
     for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<L>(partials, k));
@@ -485,25 +496,25 @@ MBLS_DEV RFq2 one_std<RFq2>() {
     return {one_std<RFq>(), RFq::zero()};
 }
 
-// one row per point (a Fermat inversion is a ~570-product serial chain)
+// one lane per point: the inversion is the binary extended Euclid of mbls_field.hpp (word
+// shifts and adds at the full VALU rate; the row-sliced Fermat chain it replaces took 0.29 ms)
 template <class F>
 __global__ void k_jac_to_icicle(uint8_t* pts, int count) {
-    using RF = typename RowOf<F>::type;
-    const int i = (int)row_id();
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (i >= count) return;
-    RJac<F> p = rload_jac<F>(pts, i);
-    RJac<F> o;
+    Jacobian<F> p = load_jac<F>(pts, i);
+    Jacobian<F> o;
     if (p.is_inf()) {
-        o.x = RF::zero();
-        o.y = one_std<RF>();
-        o.z = RF::zero();
+        o.x = F::zero();
+        o.y = one_std<F>();
+        o.z = F::zero();
     } else {
-        Affine<RF> a = jac_to_affine(p);
+        Affine<F> a = jac_to_affine(p);
         o.x = from_mont_f(a.x);
         o.y = from_mont_f(a.y);
-        o.z = one_std<RF>();
+        o.z = one_std<F>();
     }
-    rstore_jac<F>(pts, i, o);
+    store_jac<F>(pts, i, o);
 }
 
 template <class F>
@@ -587,9 +598,10 @@ struct GroupTraits<Fq2> {
 struct MsmScratchSizes {
     size_t dsrc, keys, vals, ranks, sorted, words, tmp, owner, first, partials, buckets, levelT, levelR, sums, windows, treetmp, phi;
     size_t ent, segtab, parts;  // partitioned sort (keys / vals / ranks are 0 then)
+    size_t order, perm;         // k_bucket_order: bin histograms / their scan, bucket permutation
     size_t total() const {
         return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + first + partials + buckets + levelT + levelR + sums + windows +
-               2 * TREE_SIDES * treetmp + phi + ent + 2 * segtab + 2 * parts;
+               2 * TREE_SIDES * treetmp + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm;
     }
 };
 
@@ -642,9 +654,11 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     z.dsrc = align_up(digits_src_bytes((uint32_t)(P.split > 1 ? P.pts / P.split : P.pts / P.F), P.split));
     z.sorted = align_up(NC * 4);
     z.words = align_up(((size_t)P.TB + 1) * 4);
-    z.tmp = align_up(scan_tmp_words(max_chunks > P.TB ? max_chunks : P.TB) * 4);
+    z.order = align_up(((size_t)order_words(P.TB) + 1) * 4);
+    z.perm = align_up((size_t)P.TB * 4);
+    z.tmp = align_up(scan_tmp_words(std::max(std::max(max_chunks, P.TB), order_words(P.TB))) * 4);
     z.owner = align_up((size_t)max_chunks * 4);
-    z.first = align_up((NC / CHUNK + 2) * 4);
+    z.first = align_up((NC / P.chunk + 2) * 4);
     z.partials = align_up((size_t)max_chunks * jac);
     z.buckets = align_up((size_t)P.TB * jac);
     size_t lv = 0, maxblk = 1;
@@ -659,6 +673,56 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     z.windows = align_up((size_t)P.Wg * jac);
     z.treetmp = align_up(maxblk * P.Wg * jac);
     return z;
+}
+
+inline bool debug_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("MBLS_DEBUG");
+        return e && atoi(e) != 0;
+    }();
+    return v;
+}
+
+// the accumulation kernel instance: G1 at <= 168 VGPRs (3 waves per SIMD, MBLS_ACC_W3=0: 1)
+using AccKernel = void (*)(const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, const uint8_t*,
+                           const uint8_t*, uint32_t, uint32_t, uint8_t*);
+template <class F>
+inline AccKernel accumulate_kernel() {
+    static const int w3 = [] {
+        const char* e = getenv("MBLS_ACC_W3");
+        return e ? atoi(e) : 1;
+    }();
+    if (std::is_same<F, Fq>::value && w3) return k_accumulate<F, 3>;
+    return k_accumulate<F, 1>;
+}
+
+// contributions per accumulation thread.  Default CHUNK (16): measured against spreading NC over
+// one round of resident waves (MBLS_ACC_CHUNK=auto, 86 at G1 2^20) the longer chunks cut the
+// bucket sums (0.61 -> 0.19 ms) but cost more in the accumulation (3.25 -> 3.66 ms): a chunk's
+// first addition is free when the whole wave starts a chunk together (acc = P, counter-checked:
+// SQ_INSTS_VALU +5.2% at 86), and the rest of the gap is not explained by instruction counts
+// (DESIGN.md section 8).  MBLS_ACC_CHUNK=<n> fixes it (A/B runs).
+template <class F>
+inline uint32_t accumulate_chunk(size_t NC) {
+    static const long fixed = [] {
+        const char* e = getenv("MBLS_ACC_CHUNK");
+        if (!e) return (long)CHUNK;
+        return strcmp(e, "auto") == 0 ? 0L : atol(e);
+    }();
+    if (fixed > 0) return (uint32_t)fixed;
+    static const size_t resident = [] {
+        int dev = 0, cus = 0, blocks = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(accumulate_kernel<F>()),
+                                                         256, 0) != hipSuccess ||
+            cus <= 0 || blocks <= 0)
+            return (size_t)0;
+        return (size_t)cus * blocks * 256 / LaneOf<F>::LANES;  // chains resident at once
+    }();
+    if (!resident) return CHUNK;
+    const size_t L = (NC + resident - 1) / resident;
+    return (uint32_t)std::max<size_t>(CHUNK, L);
 }
 
 // Core MSM on device operands: scalars (standard or Montgomery), bases Montgomery affine
@@ -678,7 +742,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     }
     const uint32_t TB = P.TB;
     const size_t NC = P.contributions;
-    const uint32_t max_chunks = (uint32_t)(NC / CHUNK + TB + 1);
+    const uint32_t max_chunks = (uint32_t)(NC / P.chunk + TB + 1);
     MsmScratchSizes z = msm_scratch_sizes(P, JAC, AFF, max_chunks);
     uint32_t* keys = (uint32_t*)arena.take(z.keys);
     uint32_t* vals = (uint32_t*)arena.take(z.vals);
@@ -708,7 +772,10 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint32_t* seg_cnt = (uint32_t*)arena.take(z.segtab);
     uint32_t* part_tot = (uint32_t*)arena.take(z.parts);
     uint32_t* part_base = (uint32_t*)arena.take(z.parts);
-    if (!tree_tmp[TREE_SIDES - 1][1] || (P.split > 1 && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
+    uint32_t* binhist = (uint32_t*)arena.take(z.order);
+    uint32_t* binbase = (uint32_t*)arena.take(z.order);
+    uint32_t* perm = (uint32_t*)arena.take(z.perm);
+    if (!perm || !tree_tmp[TREE_SIDES - 1][1] || (P.split > 1 && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
@@ -742,31 +809,24 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         } else if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) {
             return er;
         }
-        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, st)) != MBLS_SUCCESS) return er;
         if ((er = scan_exclusive(nchunks, chunk_off, TB, tmp, st)) != MBLS_SUCCESS) return er;
         if (!psort && (er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
-        if ((er = launch_chunk_owner(chunk_off, offsets, TB, owner, first, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_chunk_owner(chunk_off, offsets, TB, P.chunk, owner, first, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_bucket_order(nchunks, TB, binhist, binbase, tmp, perm, st)) != MBLS_SUCCESS) return er;
     }
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
         ProfScope ps("msm.accumulate", st);
         if (P.split > 1) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
-        const uint32_t threads = (uint32_t)((NC + CHUNK - 1) / CHUNK) * LN;
-        static const int w3 = [] {
-            const char* e = getenv("MBLS_ACC_W3");
-            return e ? atoi(e) : 1;
-        }();
-        if (std::is_same<F, Fq>::value && w3)
-            hipLaunchKernelGGL((k_accumulate<F, 3>), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
-                               chunk_off, first, TB, bases, phi, P.split > 1 ? n : 0xffffffffu, partials);
-        else
-            hipLaunchKernelGGL((k_accumulate<F, 1>), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
-                               chunk_off, first, TB, bases, phi, P.split > 1 ? n : 0xffffffffu, partials);
+        const uint32_t threads = (uint32_t)((NC + P.chunk - 1) / P.chunk) * LN;
+        hipLaunchKernelGGL(accumulate_kernel<F>(), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
+                           chunk_off, first, TB, bases, phi, P.split > 1 ? n : 0xffffffffu, P.chunk, partials);
     }
     {
         ProfScope ps("msm.bucket_sum", st);
         // worst case: every contribution of a window group in one bucket
-        const uint32_t max_per_bucket = (uint32_t)((P.pts + CHUNK - 1) / CHUNK);
+        const uint32_t max_per_bucket = (uint32_t)((P.pts + P.chunk - 1) / P.chunk);
         // heavy buckets (> SMALL_MAX chunks; no-op passes for random inputs) on the side stream,
         // concurrently with the light ones: disjoint partials / buckets
         if (max_per_bucket > SMALL_MAX) {
@@ -779,8 +839,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
                                nchunks + TB, partials, buckets);
             MBLS_TRY(hipEventRecord(ev[3], side));
         }
-        hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB * LN + 255) / 256), dim3(256), 0, st, chunk_off, TB, partials,
-                           buckets);
+        hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB * LN + 255) / 256), dim3(256), 0, st, chunk_off, perm,
+                           binbase + order_words(TB), partials, buckets);
         if (max_per_bucket > SMALL_MAX) MBLS_TRY(hipStreamWaitEvent(st, ev[3], 0));
     }
     ProfScope ps_red("msm.reduce", st);
@@ -898,7 +958,11 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     size_t st_s = (!cfg->are_scalars_on_device) ? align_up(n * 32 * batch) : 0;
     size_t st_b = (!cfg->are_points_on_device || !pts_mont) ? align_up(nbases * AFF) : 0;
     size_t st_r = align_up(JAC * (size_t)batch);
-    uint32_t max_chunks = (uint32_t)(P.contributions / CHUNK + P.TB + 1);
+    P.chunk = accumulate_chunk<F>(P.contributions);
+    if (debug_enabled())
+        fprintf(stderr, "[mbls] msm n=%d c=%d W=%d Wg=%d split=%d TB=%u contributions=%zu chunk=%u levels=%d\n", msm_size,
+                P.c, P.W, P.Wg, P.split, P.TB, P.contributions, P.chunk, P.levels);
+    uint32_t max_chunks = (uint32_t)(P.contributions / P.chunk + P.TB + 1);
     size_t scratch = msm_scratch_sizes(P, JAC, AFF, max_chunks).total();
     er = A.reserve(st_s + st_b + st_r + scratch + 4096);
     if (er != MBLS_SUCCESS) return er;
@@ -957,7 +1021,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
         }
     }
     if (entry == MSM_ICICLE) {
-        hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch * 16 + 63) / 64), dim3(64), 0, st, d_r, batch);
+        hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch + 63) / 64), dim3(64), 0, st, d_r, batch);
         MBLS_TRY(hipGetLastError());
     }
     MBLS_TRY(hipMemcpyAsync(results, d_r, JAC * (size_t)batch,
