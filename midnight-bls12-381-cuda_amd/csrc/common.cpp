@@ -78,10 +78,22 @@ StreamCtx& stream_ctx(hipStream_t s) {
     return *it->second;
 }
 
+static bool side_priority() {
+    static const bool v = [] {
+        const char* e = getenv("MBLS_SIDE_PRIO");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 eIcicleError StreamCtx::ensure_side(size_t nevents, size_t nsides) {
     while (sides.size() < nsides) {
         hipStream_t s;
-        MBLS_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        // highest priority: the side streams carry the latency-bound tails that must not queue
+        // behind the main stream's accumulation workgroups
+        int least = 0, greatest = 0;
+        MBLS_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        MBLS_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, side_priority() ? greatest : least));
         sides.push_back(s);
     }
     while (events.size() < nevents) {

@@ -60,15 +60,21 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     p.pts = (size_t)n * (p.split > 1 ? p.split : F);  // point indices (P_i, then the images)
     p.contributions = (size_t)n * W * p.split;
     if (p.pts >= (1u << 31)) return MBLS_INVALID_ARGUMENT;
-    // reduction levels: level 0 has B inputs, level l divides by 2^seg_log[l], the last has
-    // one output.  MBLS_ROW_SEG_LOG (tuning) overrides the row-level segment length.
+    p.groups = 1;
+    return plan_levels(p, Wg);
+}
+
+// Reduction levels for launches over Wl windows: level 0 has B inputs, level l divides by
+// 2^seg_log[l], the last has one output.  A level with many segments runs one per LANE, fewer
+// one per 16-lane ROW, few one per WAVE with shorter segments.  MBLS_ROW_SEG_LOG /
+// MBLS_WSEG_LOG / MBLS_LANE_MIN (tuning) override the row / wave segment lengths and the lane
+// threshold.
+eIcicleError plan_levels(MsmPlan& p, int Wl) {
     static const int row_log = [] {
         const char* e = getenv("MBLS_ROW_SEG_LOG");
         int v = e ? atoi(e) : SEG_LOG;
         return v >= 1 && v <= 6 ? v : SEG_LOG;
     }();
-    // Level 0 runs one segment per lane; a later level with many segments one per row (16),
-    // one with few segments one per wave with shorter segments (MBLS_WSEG_LOG, tuning).
     static const int wave_log = [] {
         const char* e = getenv("MBLS_WSEG_LOG");
         // measured (G1 2^20): 2 -> reduction 1.04 ms, 4 -> 1.12 ms once the narrow levels' tree
@@ -76,13 +82,20 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
         int v = e ? atoi(e) : 2;
         return v >= 1 && v <= 6 ? v : 2;
     }();
+    // level 0 one segment per lane only with >= lane_min chains (65536 at G1 2^20 with all 8
+    // windows in one launch; a window group has fewer and its chains are latency-bound)
+    static const uint32_t lane_min = [] {
+        const char* e = getenv("MBLS_LANE_MIN");
+        return e ? (uint32_t)atoi(e) : 32768u;
+    }();
     p.levels = 0;
     uint32_t m = p.B;
     while (true) {
         if (p.levels >= MAX_LEVELS) return MBLS_INVALID_ARGUMENT;
         int lg = SEG0_LOG, mode = MODE_LANE;
-        if (p.levels > 0) {
-            const uint32_t row_chains = ((m + (1u << row_log) - 1) >> row_log) * (uint32_t)Wg;
+        const uint32_t lane_chains = ((m + (1u << SEG0_LOG) - 1) >> SEG0_LOG) * (uint32_t)Wl;
+        if (p.levels > 0 || lane_chains < lane_min) {
+            const uint32_t row_chains = ((m + (1u << row_log) - 1) >> row_log) * (uint32_t)Wl;
             mode = row_chains >= wave_min_chains() ? MODE_ROW : MODE_WAVE;
             lg = mode == MODE_ROW ? row_log : wave_log;
         }
@@ -95,6 +108,14 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
         m = mo;
     }
     return MBLS_SUCCESS;
+}
+
+// window groups: the G groups' accumulations run in turn on the main stream while each finished
+// group's tail (bucket sums, reduction, its windows' fold) runs on a side stream (msm_device)
+eIcicleError set_groups(MsmPlan& p, int G) {
+    if (G < 1 || p.Wg % G != 0 || ((size_t)(p.Wg / G) * p.B) % 256 != 0) G = 1;
+    p.groups = G;
+    return plan_levels(p, p.Wg / G);
 }
 
 // one (key, value) contribution: the histogram atomic's return value is the contribution's
@@ -996,8 +1017,15 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
 // accumulation thread does exactly L additions; a chunk crossing bucket boundaries yields one
 // partial ("segment") per bucket it touches.  Segments of bucket b: the aligned chunks that
 // overlap [off_b, off_b + cnt_b).  nchunks[m] receives the maximum (heavy-bucket passes).
+// order-histogram index of (block, bin): group-major, then bin (heaviest first: the longest
+// bucket sums start first), then block inside the group; bpg = blocks of 256 buckets per group
+MBLS_DEV uint32_t order_index(uint32_t blk, uint32_t bin, uint32_t bpg) {
+    return (blk / bpg) * (ORDER_BINS * bpg) + (SMALL_MAX - bin) * bpg + blk % bpg;
+}
+
 __global__ void k_chunk_counts(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offsets,
-                               uint32_t* __restrict__ nchunks, uint32_t m, uint32_t L, uint32_t* __restrict__ binhist) {
+                               uint32_t* __restrict__ nchunks, uint32_t m, uint32_t L, uint32_t* __restrict__ binhist,
+                               uint32_t bpg) {
     __shared__ uint32_t hist[ORDER_BINS];
     if (threadIdx.x < ORDER_BINS) hist[threadIdx.x] = 0;
     __syncthreads();
@@ -1019,17 +1047,18 @@ __global__ void k_chunk_counts(const uint32_t* __restrict__ counts, const uint32
         c = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
         if (c > 1 && c > __atomic_load_n(&nchunks[m], __ATOMIC_RELAXED)) atomicMax(&nchunks[m], c);
     }
-    // per-block histogram of the light buckets' chunk counts, bin-major (k_bucket_order)
-    if (threadIdx.x < ORDER_BINS) binhist[threadIdx.x * gridDim.x + blockIdx.x] = hist[threadIdx.x];
+    // per-block histogram of the light buckets' chunk counts (k_bucket_order)
+    if (threadIdx.x < ORDER_BINS) binhist[order_index(blockIdx.x, threadIdx.x, bpg)] = hist[threadIdx.x];
 }
 
-// perm = the light buckets (<= SMALL_MAX chunks) grouped by chunk count, so the waves of
-// k_bucket_small run uniform trip counts (bucket order alone gave ~4 +- 1.5 chunks per lane and
-// a wave ran its maximum).  binbase = exclusive scan of k_chunk_counts' bin-major histograms.
+// perm = the light buckets (<= SMALL_MAX chunks) grouped by window group, then by chunk count
+// (heaviest first), so the waves of k_bucket_small run uniform trip counts (bucket order alone
+// gave ~4 +- 1.5 chunks per lane and a wave ran its maximum).  binbase = exclusive scan of
+// k_chunk_counts' histograms (order_index layout).
 __global__ void k_bucket_order(const uint32_t* __restrict__ nchunks, uint32_t m, const uint32_t* __restrict__ binbase,
-                               uint32_t* __restrict__ perm) {
+                               uint32_t bpg, uint32_t* __restrict__ perm) {
     __shared__ uint32_t cur[ORDER_BINS];
-    if (threadIdx.x < ORDER_BINS) cur[threadIdx.x] = binbase[threadIdx.x * gridDim.x + blockIdx.x];
+    if (threadIdx.x < ORDER_BINS) cur[threadIdx.x] = binbase[order_index(blockIdx.x, threadIdx.x, bpg)];
     __syncthreads();
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
@@ -1038,9 +1067,11 @@ __global__ void k_bucket_order(const uint32_t* __restrict__ nchunks, uint32_t m,
 }
 
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
-                                 uint32_t L, uint32_t* binhist, hipStream_t st) {
+                                 uint32_t L, uint32_t* binhist, uint32_t groups, hipStream_t st) {
     MBLS_TRY(hipMemsetAsync(nchunks + m, 0, 4, st));
-    hipLaunchKernelGGL(k_chunk_counts, dim3((m + 255) / 256), dim3(256), 0, st, counts, offsets, nchunks, m, L, binhist);
+    const uint32_t nblk = (m + 255) / 256;
+    hipLaunchKernelGGL(k_chunk_counts, dim3(nblk), dim3(256), 0, st, counts, offsets, nchunks, m, L, binhist,
+                       nblk / groups);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }
@@ -1048,10 +1079,11 @@ eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets
 uint32_t order_words(uint32_t m) { return ORDER_BINS * ((m + 255) / 256); }
 
 eIcicleError launch_bucket_order(const uint32_t* nchunks, uint32_t m, const uint32_t* binhist, uint32_t* binbase,
-                                 uint32_t* tmp, uint32_t* perm, hipStream_t st) {
+                                 uint32_t* tmp, uint32_t* perm, uint32_t groups, hipStream_t st) {
     eIcicleError er = scan_exclusive(binhist, binbase, order_words(m), tmp, st);
     if (er != MBLS_SUCCESS) return er;
-    hipLaunchKernelGGL(k_bucket_order, dim3((m + 255) / 256), dim3(256), 0, st, nchunks, m, binbase, perm);
+    const uint32_t nblk = (m + 255) / 256;
+    hipLaunchKernelGGL(k_bucket_order, dim3(nblk), dim3(256), 0, st, nchunks, m, binbase, nblk / groups, perm);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }

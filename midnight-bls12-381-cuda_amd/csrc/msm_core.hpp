@@ -47,6 +47,14 @@
 namespace mbls {
 
 static constexpr uint32_t INVALID_KEY = 0xffffffffu;
+
+// Wave priority of the latency-bound tail kernels (bucket sums, reduction, folds).  With window
+// groups they run beside the next group's VALU-saturating accumulation, and the VALU issue
+// arbiter picks by priority, then age (MI355X_MICROARCH.md): raised, their chains keep issuing.
+#ifndef MBLS_SETPRIO
+#define MBLS_SETPRIO 3
+#endif
+#define MBLS_TAIL_PRIO() __builtin_amdgcn_s_setprio(MBLS_SETPRIO)
 #ifndef MBLS_CHUNK
 #define MBLS_CHUNK 16
 #endif
@@ -69,7 +77,8 @@ struct MsmPlan {
     uint32_t chunk;             // contributions per accumulation thread (accumulate_chunk)
     size_t pts;                 // distinct point indices (n, n*F, or split*n)
     size_t contributions;
-    int levels;                 // bucket-reduction levels
+    int groups;                 // window groups pipelined across streams (set_groups; 1 = one pass)
+    int levels;                 // bucket-reduction levels (of one group's launch: Wg / groups windows)
     uint32_t level_m[MAX_LEVELS];  // inputs per window at each level
     uint8_t seg_log[MAX_LEVELS];   // log2 segment length per level
     uint8_t mode[MAX_LEVELS];      // MODE_LANE / MODE_ROW / MODE_WAVE per level
@@ -83,6 +92,8 @@ struct MsmPlan {
 
 // endo: the split the group offers (1 none, 2 G1 GLV, 4 G2 psi); make_plan decides whether to use it
 eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo = 1);
+eIcicleError plan_levels(MsmPlan& p, int Wl);
+eIcicleError set_groups(MsmPlan& p, int G);
 // bits between consecutive multiples in a precomputed table: [P, 2^s P, 2^(2s) P, ...], s = ceil(256 / F)
 int precompute_shift(int F);
 
@@ -92,9 +103,9 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
 size_t digits_src_bytes(uint32_t n, int split);
 eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint32_t* tmp, hipStream_t st);
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
-                                 uint32_t L, uint32_t* binhist, hipStream_t st);
+                                 uint32_t L, uint32_t* binhist, uint32_t groups, hipStream_t st);
 eIcicleError launch_bucket_order(const uint32_t* nchunks, uint32_t m, const uint32_t* binhist, uint32_t* binbase,
-                                 uint32_t* tmp, uint32_t* perm, hipStream_t st);
+                                 uint32_t* tmp, uint32_t* perm, uint32_t groups, hipStream_t st);
 uint32_t order_words(uint32_t m);
 eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const uint32_t* ranks, size_t total,
                             const uint32_t* offsets, uint32_t* sorted, hipStream_t st);
@@ -132,16 +143,20 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
 template <class F, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ chunk_off,
-                                                    const uint32_t* __restrict__ first, uint32_t TB,
+                                                    const uint32_t* __restrict__ first, uint32_t b0, uint32_t b1,
                                                     const uint8_t* __restrict__ bases, const uint8_t* __restrict__ phi,
                                                     uint32_t nsplit, uint32_t chunk, uint8_t* __restrict__ partials) {
     using L = typename LaneOf<F>::type;
-    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
-    const uint32_t total = offsets[TB];
-    const uint32_t beg = t * chunk;
-    if (beg >= total) return;
-    const uint32_t end = min(beg + chunk, total);
+    // buckets [b0, b1) only (one window group): sorted positions [offsets[b0], offsets[b1]); a
+    // chunk straddling the group boundary is shared, each side summing its own positions
+    const uint32_t gb = offsets[b0], ge = offsets[b1];
+    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES + gb / chunk;  // chunk index
+    uint32_t beg = t * chunk;
+    const uint32_t end = min(beg + chunk, ge);
+    beg = max(beg, gb);
+    if (beg >= end) return;
     uint32_t b = first[t];
+    while (offsets[b + 1] <= beg) ++b;  // straddling chunk: the group's first non-empty bucket
     uint32_t seg = chunk_off[b] + (t - offsets[b] / chunk);
     uint32_t bend = offsets[b + 1];
     Jacobian<L> acc = Jacobian<L>::inf();
@@ -207,15 +222,17 @@ static constexpr int TREE_FANIN = 8;
 
 template <class F>
 __global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict__ chunk_off,
-                                                     const uint32_t* __restrict__ owner, uint32_t TB,
+                                                     const uint32_t* __restrict__ owner, uint32_t b0, uint32_t b1,
                                                      uint32_t max_chunks, const uint32_t* __restrict__ maxc,
                                                      uint32_t step, uint8_t* __restrict__ partials) {
+    MBLS_TAIL_PRIO();
     using L = typename LaneOf<F>::type;
     constexpr uint32_t LN = LaneOf<F>::LANES;
     if (*maxc <= SMALL_MAX || step >= *maxc) return;  // only heavy buckets remain
-    const uint32_t total = min(max_chunks, chunk_off[TB]);
+    const uint32_t total = min(max_chunks, chunk_off[b1]);
     // capped grid, grid-stride: a pass that finds no work costs one small launch
-    for (uint32_t ch = (blockIdx.x * blockDim.x + threadIdx.x) / LN; ch < total; ch += gridDim.x * blockDim.x / LN) {
+    for (uint32_t ch = chunk_off[b0] + (blockIdx.x * blockDim.x + threadIdx.x) / LN; ch < total;
+         ch += gridDim.x * blockDim.x / LN) {
         const uint32_t b = owner[ch];
         const uint32_t j = ch - chunk_off[b];
         const uint32_t cnt = chunk_off[b + 1] - chunk_off[b];
@@ -232,18 +249,23 @@ __global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict_
 }
 
 // common case: one thread per light bucket (<= SMALL_MAX chunks) sums its chunk partials;
-// thread t takes perm[t] (k_bucket_order: buckets grouped by chunk count, so a wave's lanes run
-// the same number of additions).  nlight = the order scan's total.
+// thread t of window group g takes perm[start_g + t] (k_bucket_order: buckets grouped by group,
+// then by chunk count, so a wave's lanes run the same number of additions).  The group's range
+// of perm comes from the order scan: binbase at the group's first histogram word, and the next
+// group's (the scan total for the last group).
 template <class F>
 #ifndef MBLS_BS_MINW
 #define MBLS_BS_MINW 1
 #endif
 __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32_t* __restrict__ chunk_off,
-                                                      const uint32_t* __restrict__ perm, const uint32_t* __restrict__ nlight,
-                                                      const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
+                                                      const uint32_t* __restrict__ perm, const uint32_t* __restrict__ binbase,
+                                                      uint32_t g, uint32_t gwords, const uint8_t* __restrict__ partials,
+                                                      uint8_t* __restrict__ buckets) {
+    MBLS_TAIL_PRIO();
     using L = typename LaneOf<F>::type;
-    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
-    if (t >= *nlight) return;
+    const uint32_t start = binbase[g * gwords], stop = binbase[(g + 1) * gwords];
+    const uint32_t t = start + (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
+    if (t >= stop) return;
     const uint32_t b = perm[t];
     const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
     Jacobian<L> acc = Jacobian<L>::inf();
@@ -253,12 +275,12 @@ __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32
 }
 
 template <class F>
-__global__ __launch_bounds__(256) void k_bucket_gather(const uint32_t* __restrict__ chunk_off, uint32_t m,
+__global__ __launch_bounds__(256) void k_bucket_gather(const uint32_t* __restrict__ chunk_off, uint32_t b0, uint32_t b1,
                                                        const uint32_t* __restrict__ maxc,
                                                        const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
     if (*maxc <= SMALL_MAX) return;
-    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= m) return;
+    uint32_t b = b0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= b1) return;
     const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
     if (k1 - k0 > SMALL_MAX) store_jac<F>(buckets, b, load_jac<F>(partials, k0));
 }
@@ -337,6 +359,7 @@ constexpr uint32_t lanes_per_chain() { return MODE == MODE_LANE ? 1u : MODE == M
 template <class F, int MODE>
 __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict__ V, uint32_t m_in, uint32_t seg, int Wg,
                                                       int off, uint8_t* __restrict__ T, uint8_t* __restrict__ R) {
+    MBLS_TAIL_PRIO();
     using IO = RedIO<F, MODE>;
     using J = typename IO::J;
     const uint32_t m_out = (m_in + seg - 1) / seg;
@@ -397,6 +420,7 @@ MBLS_DEV void tree_sum_block(const uint8_t* __restrict__ V, uint32_t m, uint32_t
 template <class F>
 __global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V, uint32_t m, uint32_t nblk,
                                                   uint8_t* __restrict__ out) {
+    MBLS_TAIL_PRIO();
     tree_sum_block<F>(V, m, blockIdx.x / nblk, blockIdx.x % nblk, TREE_PER_ROW, out, blockIdx.x);
 }
 
@@ -412,6 +436,7 @@ struct TreeJobs {
 };
 template <class F>
 __global__ __launch_bounds__(256) void k_tree_sum_jobs(TreeJobs jobs, int Wg) {
+    MBLS_TAIL_PRIO();
     const uint32_t j = blockIdx.x / Wg, w = blockIdx.x % Wg;
     tree_sum_block<F>(jobs.V[j], jobs.m[j], w, 0, (jobs.m[j] + 15) / 16, jobs.out[j], w);
 }
@@ -420,6 +445,7 @@ __global__ __launch_bounds__(256) void k_tree_sum_jobs(TreeJobs jobs, int Wg) {
 template <class F, int MODE>
 __global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, int Wg, uint64_t seg_logs,
                                 uint8_t* __restrict__ windows) {
+    MBLS_TAIL_PRIO();
     using IO = RedIO<F, MODE>;
     const int w = (int)IO::id();
     if (w >= Wg) return;
@@ -435,6 +461,7 @@ __global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, in
 // final fold over window groups: sum_w 2^(c w) G_w  (one chain)
 template <class F, int MODE>
 __global__ void k_final(const uint8_t* __restrict__ windows, int Wg, int c, uint8_t* __restrict__ result) {
+    MBLS_TAIL_PRIO();
     using IO = RedIO<F, MODE>;
     if (IO::id() != 0) return;
     auto acc = IO::ld(windows, Wg - 1);
@@ -443,6 +470,27 @@ __global__ void k_final(const uint8_t* __restrict__ windows, int Wg, int c, uint
         acc = IO::add(acc, IO::ld(windows, w));
     }
     IO::st(result, 0, acc);
+}
+
+// window-group fold chain (msm_device, groups > 1): acc = 2^ndbl acc, then acc += H_g (acc = H_g
+// for the first group); the doublings only wait for the previous fold, not for group g's tail
+template <class F>
+__global__ void k_fold_dbl(uint8_t* __restrict__ acc, int ndbl) {
+    MBLS_TAIL_PRIO();
+    using IO = RedIO<F, MODE_WAVE>;
+    if (IO::id() != 0) return;
+    auto a = IO::ld(acc, 0);
+    for (int k = 0; k < ndbl; ++k) a = IO::dbl(a);
+    IO::st(acc, 0, a);
+}
+template <class F>
+__global__ void k_fold_add(uint8_t* __restrict__ acc, const uint8_t* __restrict__ h, int first) {
+    MBLS_TAIL_PRIO();
+    using IO = RedIO<F, MODE_WAVE>;
+    if (IO::id() != 0) return;
+    auto a = IO::ld(h, 0);
+    if (!first) a = IO::add(IO::ld(acc, 0), a);
+    IO::st(acc, 0, a);
 }
 
 template <class F>
@@ -599,9 +647,10 @@ struct MsmScratchSizes {
     size_t dsrc, keys, vals, ranks, sorted, words, tmp, owner, first, partials, buckets, levelT, levelR, sums, windows, treetmp, phi;
     size_t ent, segtab, parts;  // partitioned sort (keys / vals / ranks are 0 then)
     size_t order, perm;         // k_bucket_order: bin histograms / their scan, bucket permutation
+    size_t gsum;                // window groups' folds H_g
     size_t total() const {
         return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + first + partials + buckets + levelT + levelR + sums + windows +
-               2 * TREE_SIDES * treetmp + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm;
+               2 * TREE_SIDES * treetmp + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm + gsum;
     }
 };
 
@@ -671,6 +720,7 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     z.levelR = align_up(lv * P.Wg * jac);
     z.sums = align_up((size_t)P.levels * P.Wg * jac);
     z.windows = align_up((size_t)P.Wg * jac);
+    z.gsum = align_up((size_t)P.groups * jac);
     z.treetmp = align_up(maxblk * P.Wg * jac);
     return z;
 }
@@ -684,8 +734,8 @@ inline bool debug_enabled() {
 }
 
 // the accumulation kernel instance: G1 at <= 168 VGPRs (3 waves per SIMD, MBLS_ACC_W3=0: 1)
-using AccKernel = void (*)(const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, const uint8_t*,
-                           const uint8_t*, uint32_t, uint32_t, uint8_t*);
+using AccKernel = void (*)(const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, uint32_t,
+                           const uint8_t*, const uint8_t*, uint32_t, uint32_t, uint8_t*);
 template <class F>
 inline AccKernel accumulate_kernel() {
     static const int w3 = [] {
@@ -723,6 +773,82 @@ inline uint32_t accumulate_chunk(size_t NC) {
     if (!resident) return CHUNK;
     const size_t L = (NC + resident - 1) / resident;
     return (uint32_t)std::max<size_t>(CHUNK, L);
+}
+
+// one reduction level over Wl windows (weights t + off; off = 1 at level 0: bucket t holds digit t + 1)
+template <class F>
+inline void launch_reduce_level(int mode, const uint8_t* V, uint32_t m_in, uint32_t seg, int Wl, int off, uint8_t* T,
+                                uint8_t* R, uint32_t chains, hipStream_t s) {
+    constexpr uint32_t LN = LaneOf<F>::LANES;
+    if (mode == MODE_LANE)  // one segment per lane
+        hipLaunchKernelGGL((k_reduce_level<F, MODE_LANE>), dim3((chains * LN + 255) / 256), dim3(256), 0, s, V, m_in, seg,
+                           Wl, off, T, R);
+    else if (mode == MODE_ROW)  // many segments: one per 16-lane row
+        hipLaunchKernelGGL((k_reduce_level<F, MODE_ROW>), dim3((chains * 16 + 255) / 256), dim3(256), 0, s, V, m_in, seg,
+                           Wl, off, T, R);
+    else  // few segments: one per wave (latency-bound chains)
+        hipLaunchKernelGGL((k_reduce_level<F, MODE_WAVE>), dim3((chains * 64 + 255) / 256), dim3(256), 0, s, V, m_in, seg,
+                           Wl, off, T, R);
+}
+
+// bucket reduction of one window group (Wl windows, group g) on one stream: the levels, each
+// level's T sum (tree stages in line, narrow levels batched into one launch), the window Horner.
+// V = the group's buckets; level l's outputs live at [lvoff_l * Wg + g * Wl * m_out_l) of the
+// level arrays (all groups side by side); sums / windows point at the group's slices.
+template <class F>
+eIcicleError reduce_windows(const MsmPlan& P, const uint8_t* V, int Wl, int g, uint8_t* levelT, uint8_t* levelR,
+                            uint8_t* sums, uint8_t* windows, uint8_t* const (&tt)[2], hipStream_t s) {
+    constexpr size_t JAC = GroupTraits<F>::JAC;
+    size_t lvoff = 0;
+    TreeJobs jobs;
+    int njobs = 0;
+    for (int l = 0; l < P.levels; ++l) {
+        const uint32_t m_in = P.level_m[l], seg = P.seg(l);
+        const uint32_t m_out = (m_in + seg - 1) / seg;
+        const size_t at = (lvoff * P.Wg + (size_t)g * Wl * m_out) * JAC;
+        uint8_t* T = levelT + at;
+        uint8_t* R = levelR + at;
+        launch_reduce_level<F>(P.mode[l], V, m_in, seg, Wl, l == 0 ? 1 : 0, T, R, m_out * (uint32_t)Wl, s);
+        if (m_out <= TREE_DEFER_POINTS) {
+            jobs.V[njobs] = T;
+            jobs.m[njobs] = m_out;
+            jobs.out[njobs] = sums + (size_t)l * Wl * JAC;
+            ++njobs;
+        } else {
+            const uint8_t* src = T;
+            uint32_t m = m_out;
+            int flip = 0;
+            while (true) {
+                const uint32_t nblk = tree_blocks(m);
+                uint8_t* dst = nblk == 1 ? sums + (size_t)l * Wl * JAC : tt[flip];
+                hipLaunchKernelGGL(k_tree_sum<F>, dim3(Wl * nblk), dim3(256), 0, s, src, m, nblk, dst);
+                if (nblk == 1) break;
+                src = dst;
+                m = nblk;
+                flip ^= 1;
+            }
+        }
+        V = R;
+        lvoff += m_out;
+    }
+    if (njobs) hipLaunchKernelGGL(k_tree_sum_jobs<F>, dim3(njobs * Wl), dim3(256), 0, s, jobs, Wl);
+    hipLaunchKernelGGL((k_window_horner<F, MODE_WAVE>), dim3(Wl), dim3(64), 0, s, sums, P.levels, Wl, P.seg_logs_packed(),
+                       windows);
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
+}
+
+// window groups for one MSM (MBLS_GROUPS; default 1 = one pass over all windows).  Measured
+// at G1 2^20: 2 / 4 / 8 groups 171 / 165 / 125 MSM/s against 191 for one
+// pass -- the tails are latency-bound row / wave-sliced chains that cost ~4x the VALU issue per
+// product of the lane-sliced accumulation, so beside it they slow the accumulation (3.27 ->
+// 4.15 ms summed over 4 groups) more than they hide.
+inline int msm_groups() {
+    static const int v = [] {
+        const char* e = getenv("MBLS_GROUPS");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
 }
 
 // Core MSM on device operands: scalars (standard or Montgomery), bases Montgomery affine
@@ -775,13 +901,17 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint32_t* binhist = (uint32_t*)arena.take(z.order);
     uint32_t* binbase = (uint32_t*)arena.take(z.order);
     uint32_t* perm = (uint32_t*)arena.take(z.perm);
-    if (!perm || !tree_tmp[TREE_SIDES - 1][1] || (P.split > 1 && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
+    uint8_t* gsum = (uint8_t*)arena.take(z.gsum);
+    if (!gsum || !tree_tmp[TREE_SIDES - 1][1] || (P.split > 1 && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
     // side stream: the phi(P) table and the heavy-bucket passes overlap the main chain; the
     // per-level tree sums of the reduction run there too.  Events [levels+1 ..) fork / join.
-    if ((er = ctx.ensure_side((size_t)P.levels + 5 + TREE_SIDES, TREE_SIDES)) != MBLS_SUCCESS) return er;
+    // events: [0, levels] tree forks / join, [levels + 1, +8 + TREE_SIDES) table / heavy / joins,
+    // then 2 groups + 1 for the window-group pipeline (all ensured here: `ev` must stay valid)
+    if ((er = ctx.ensure_side((size_t)P.levels + 8 + TREE_SIDES + 2 * (size_t)P.groups + 1, TREE_SIDES)) != MBLS_SUCCESS)
+        return er;
     hipStream_t side = use_side ? ctx.sides[0] : st;
     hipEvent_t* ev = ctx.events.data() + P.levels + 1;
     if (P.split > 1) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
@@ -809,11 +939,67 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         } else if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) {
             return er;
         }
-        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, P.groups, st)) != MBLS_SUCCESS)
+            return er;
         if ((er = scan_exclusive(nchunks, chunk_off, TB, tmp, st)) != MBLS_SUCCESS) return er;
         if (!psort && (er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
         if ((er = launch_chunk_owner(chunk_off, offsets, TB, P.chunk, owner, first, st)) != MBLS_SUCCESS) return er;
-        if ((er = launch_bucket_order(nchunks, TB, binhist, binbase, tmp, perm, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_bucket_order(nchunks, TB, binhist, binbase, tmp, perm, P.groups, st)) != MBLS_SUCCESS) return er;
+    }
+    // worst case: every contribution of a window in one bucket
+    const uint32_t max_per_bucket = (uint32_t)((P.pts + P.chunk - 1) / P.chunk);
+    const uint32_t nsplit = P.split > 1 ? n : 0xffffffffu;
+    if (P.groups > 1 && use_side) {
+        // ---- window groups: group g's accumulation on the main stream, then its tail (bucket
+        // sums, reduction, fold of its windows) on a side stream while group g-1 accumulates;
+        // the groups' folds H_g are combined top-down on a third stream, acc = 2^(c Wpg) acc +
+        // H_g, its doublings waiting only for the previous fold.  Only the last group's tail
+        // and one fold step remain after the last accumulation.
+        const int G = P.groups, Wpg = P.Wg / G;
+        const uint32_t Bg = (uint32_t)Wpg * P.B;
+        const uint32_t gwords = order_words(TB) / (uint32_t)G;
+        const size_t gev0 = (size_t)P.levels + 8 + TREE_SIDES;
+        hipEvent_t* gev = ctx.events.data() + gev0;  // [0, G) accumulated, [G, 2G) tail done, 2G folded
+        hipStream_t comb = ctx.sides[2];
+        const uint32_t gthreads = (uint32_t)((NC / G + P.chunk - 1) / P.chunk + 2) * LN;
+        if (P.split > 1) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
+        for (int k = 0; k < G; ++k) {
+            const int g = G - 1 - k;  // top windows first: the fold is a Horner from the top
+            const uint32_t b0 = (uint32_t)g * Bg, b1 = b0 + Bg;
+            {
+                ProfScope ps("msm.accumulate", st);
+                hipLaunchKernelGGL(accumulate_kernel<F>(), dim3((gthreads + 255) / 256), dim3(256), 0, st, sorted,
+                                   offsets, chunk_off, first, b0, b1, bases, phi, nsplit, P.chunk, partials);
+            }
+            MBLS_TRY(hipEventRecord(gev[g], st));
+            hipStream_t ts = ctx.sides[k & 1];
+            MBLS_TRY(hipStreamWaitEvent(ts, gev[g], 0));
+            if (max_per_bucket > SMALL_MAX) {  // heavy buckets (no-op passes for random inputs)
+                for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
+                    hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN / G + 255) / 256, 1024u)),
+                                       dim3(256), 0, ts, chunk_off, owner, b0, b1, max_chunks, nchunks + TB, step, partials);
+                hipLaunchKernelGGL(k_bucket_gather<F>, dim3((Bg + 255) / 256), dim3(256), 0, ts, chunk_off, b0, b1,
+                                   nchunks + TB, partials, buckets);
+            }
+            hipLaunchKernelGGL(k_bucket_small<F>, dim3((Bg * LN + 255) / 256), dim3(256), 0, ts, chunk_off, perm, binbase,
+                               (uint32_t)g, gwords, partials, buckets);
+            if ((er = reduce_windows<F>(P, buckets + (size_t)b0 * JAC, Wpg, g, levelT, levelR, sums + (size_t)g * P.levels * Wpg * JAC,
+                                        windows + (size_t)g * Wpg * JAC, tree_tmp[k & 1], ts)) != MBLS_SUCCESS)
+                return er;
+            hipLaunchKernelGGL((k_final<F, MODE_WAVE>), dim3(1), dim3(64), 0, ts, windows + (size_t)g * Wpg * JAC, Wpg, P.c,
+                               gsum + (size_t)g * JAC);
+            MBLS_TRY(hipEventRecord(gev[G + g], ts));
+            if (k > 0) hipLaunchKernelGGL(k_fold_dbl<F>, dim3(1), dim3(64), 0, comb, result, P.c * Wpg);
+            MBLS_TRY(hipStreamWaitEvent(comb, gev[G + g], 0));
+            hipLaunchKernelGGL(k_fold_add<F>, dim3(1), dim3(64), 0, comb, result, gsum + (size_t)g * JAC, k == 0 ? 1 : 0);
+        }
+        MBLS_TRY(hipEventRecord(gev[2 * G], comb));
+        {
+            ProfScope ps("msm.tail", st);  // exposed tail: last accumulation -> fold done
+            MBLS_TRY(hipStreamWaitEvent(st, gev[2 * G], 0));
+        }
+        MBLS_TRY(hipGetLastError());
+        return MBLS_SUCCESS;
     }
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
@@ -821,12 +1007,10 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         if (P.split > 1) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
         const uint32_t threads = (uint32_t)((NC + P.chunk - 1) / P.chunk) * LN;
         hipLaunchKernelGGL(accumulate_kernel<F>(), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
-                           chunk_off, first, TB, bases, phi, P.split > 1 ? n : 0xffffffffu, P.chunk, partials);
+                           chunk_off, first, 0u, TB, bases, phi, nsplit, P.chunk, partials);
     }
     {
         ProfScope ps("msm.bucket_sum", st);
-        // worst case: every contribution of a window group in one bucket
-        const uint32_t max_per_bucket = (uint32_t)((P.pts + P.chunk - 1) / P.chunk);
         // heavy buckets (> SMALL_MAX chunks; no-op passes for random inputs) on the side stream,
         // concurrently with the light ones: disjoint partials / buckets
         if (max_per_bucket > SMALL_MAX) {
@@ -834,13 +1018,13 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             MBLS_TRY(hipStreamWaitEvent(side, ev[2], 0));
             for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
                 hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN + 255) / 256, 1024u)), dim3(256), 0, side, chunk_off,
-                                   owner, TB, max_chunks, nchunks + TB, step, partials);
-            hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, side, chunk_off, TB,
+                                   owner, 0u, TB, max_chunks, nchunks + TB, step, partials);
+            hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, side, chunk_off, 0u, TB,
                                nchunks + TB, partials, buckets);
             MBLS_TRY(hipEventRecord(ev[3], side));
         }
-        hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB * LN + 255) / 256), dim3(256), 0, st, chunk_off, perm,
-                           binbase + order_words(TB), partials, buckets);
+        hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB * LN + 255) / 256), dim3(256), 0, st, chunk_off, perm, binbase,
+                           0u, order_words(TB), partials, buckets);
         if (max_per_bucket > SMALL_MAX) MBLS_TRY(hipStreamWaitEvent(st, ev[3], 0));
     }
     ProfScope ps_red("msm.reduce", st);
@@ -859,16 +1043,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         uint8_t* T = levelT + lvoff * JAC;
         uint8_t* R = levelR + lvoff * JAC;
         const uint32_t chains = m_out * (uint32_t)P.Wg;
-        if (P.mode[l] == MODE_LANE) {  // one segment per lane
-            hipLaunchKernelGGL((k_reduce_level<F, MODE_LANE>), dim3((chains * LN + 255) / 256), dim3(256), 0, st, V, m_in,
-                               seg, P.Wg, 1, T, R);
-        } else if (P.mode[l] == MODE_ROW) {  // many segments: one per 16-lane row
-            hipLaunchKernelGGL((k_reduce_level<F, MODE_ROW>), dim3((chains * 16 + 255) / 256), dim3(256), 0, st, V,
-                               m_in, seg, P.Wg, 0, T, R);
-        } else {  // few segments: one per wave (latency-bound chains)
-            hipLaunchKernelGGL((k_reduce_level<F, MODE_WAVE>), dim3((chains * 64 + 255) / 256), dim3(256), 0, st, V,
-                               m_in, seg, P.Wg, 0, T, R);
-        }
+        launch_reduce_level<F>(P.mode[l], V, m_in, seg, P.Wg, l == 0 ? 1 : 0, T, R, chains, st);
         // sum of this level's T per window: narrow levels are batched after the last level;
         // wide ones run tree stages on the side stream, overlapped with the next levels
         if (m_out <= TREE_DEFER_POINTS && defer_narrow_trees()) {
@@ -959,6 +1134,10 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     size_t st_b = (!cfg->are_points_on_device || !pts_mont) ? align_up(nbases * AFF) : 0;
     size_t st_r = align_up(JAC * (size_t)batch);
     P.chunk = accumulate_chunk<F>(P.contributions);
+    // window groups pipeline one MSM's tails behind its own accumulations (side streams); the
+    // pipelined batch members already overlap each other's tails and run without side streams
+    er = set_groups(P, batch >= 2 && batch_pipeline() ? 1 : msm_groups());
+    if (er != MBLS_SUCCESS) return er;
     if (debug_enabled())
         fprintf(stderr, "[mbls] msm n=%d c=%d W=%d Wg=%d split=%d TB=%u contributions=%zu chunk=%u levels=%d\n", msm_size,
                 P.c, P.W, P.Wg, P.split, P.TB, P.contributions, P.chunk, P.levels);
