@@ -164,9 +164,49 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ 
     }
     __syncthreads();
 
-    // ---- L radix-2 DIT stages
+    // ---- L DIT stages: pairs of stages as radix-4 (2 x 2) butterflies in registers (one LDS
+    // round trip and one barrier per pair), an odd last stage as radix-2
     const size_t lo_base = FIRST ? 0 : (size_t)(tile % (int)(((size_t)1 << s0) >> logC)) * C;
-    for (int l = 1; l <= L; ++l) {
+    int l = 1;
+    for (; l + 1 <= L; l += 2) {
+        const int h = 1 << (l - 1);  // stage l pairs rows (t, t + h), stage l + 1 rows (t, t + 2h)
+        const int s = s0 + l;        // global stage of the first of the pair
+        const uint8_t* tw1 = tw + 32 * (((size_t)1 << (s - 1)) - 1);
+        const uint8_t* tw2 = tw + 32 * (((size_t)1 << s) - 1);
+        for (int u = threadIdx.x; u < T / 4; u += NTT_THREADS) {
+            const int c = u & (C - 1);
+            const int r = u >> logC;
+            const int j = r & (h - 1);
+            const int q = ((r >> (l - 1)) << (l + 1)) + j;
+            uint8_t* p0 = lds + 32 * (q * C + c);
+            const size_t stride = (size_t)32 * h * C;
+            Fr x0 = load<FrCfg>(p0), x1 = load<FrCfg>(p0 + stride), x2 = load<FrCfg>(p0 + 2 * stride),
+               x3 = load<FrCfg>(p0 + 3 * stride);
+            const size_t lo = FIRST ? 0 : lo_base + c;
+            // stage l: (x0, x1), (x2, x3) share twiddle w_(2^s)^j; trivial for j = 0 in the first
+            // pass (always at s = 1: h = 1)
+            if (!(FIRST && l == 1)) {
+                const Fr w1 = load<FrCfg>(tw1 + 32 * (((size_t)j << s0) + lo));
+                x1 = fips::mul<FrCfg, false>(x1, w1);
+                x3 = fips::mul<FrCfg, false>(x3, w1);
+            }
+            Fr y0 = add_2r(x0, x1), y1 = sub_2r(x0, x1), y2 = add_2r(x2, x3), y3 = sub_2r(x2, x3);
+            // stage l + 1: (y0, y2) with w_(2^(s+1))^j (trivial in the first pair of the first
+            // pass: j = 0), (y1, y3) with w_(2^(s+1))^(j + h)
+            if (!(FIRST && l == 1)) {
+                const Fr w2 = load<FrCfg>(tw2 + 32 * (((size_t)j << s0) + lo));
+                y2 = fips::mul<FrCfg, false>(y2, w2);
+            }
+            const Fr w3 = load<FrCfg>(tw2 + 32 * (((size_t)(j + h) << s0) + lo));
+            y3 = fips::mul<FrCfg, false>(y3, w3);
+            store<FrCfg>(p0, add_2r(y0, y2));
+            store<FrCfg>(p0 + 2 * stride, sub_2r(y0, y2));
+            store<FrCfg>(p0 + stride, add_2r(y1, y3));
+            store<FrCfg>(p0 + 3 * stride, sub_2r(y1, y3));
+        }
+        __syncthreads();
+    }
+    if (l == L) {  // odd stage count: one radix-2 stage
         const int half = 1 << (l - 1);
         const int s = s0 + l;  // global stage, m = 2^s
         for (int u = threadIdx.x; u < T / 2; u += NTT_THREADS) {
