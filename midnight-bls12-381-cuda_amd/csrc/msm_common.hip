@@ -429,8 +429,9 @@ MBLS_DEV uint64_t divmod_x(uint32_t (&t)[8]) {
 
 template <bool MONT>
 __global__ __launch_bounds__(256) void k_psi_split(const uint8_t* __restrict__ scalars, uint32_t n,
-                                                   uint4* __restrict__ out) {
+                                                   uint4* __restrict__ out, ZeroList z) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    z.run(i, gridDim.x * blockDim.x);
     if (i >= n) return;
     Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
     if (MONT) s = from_mont(s);
@@ -514,8 +515,9 @@ static constexpr uint32_t DT_MAX_B = 1u << 15;
 
 template <bool MONT>
 __global__ __launch_bounds__(256) void k_glv_split(const uint8_t* __restrict__ scalars, uint32_t n,
-                                                   uint4* __restrict__ out) {
+                                                   uint4* __restrict__ out, ZeroList z) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    z.run(i, gridDim.x * blockDim.x);
     if (i >= n) return;
     Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
     if (MONT) s = from_mont(s);
@@ -526,8 +528,9 @@ __global__ __launch_bounds__(256) void k_glv_split(const uint8_t* __restrict__ s
     out[n + i] = make_uint4(m2[0], m2[1], m2[2], m2[3] | (n2 ? 0x80000000u : 0u));
 }
 
-__global__ void k_scalars_std(const uint8_t* __restrict__ scalars, uint32_t n, uint8_t* __restrict__ out) {
+__global__ void k_scalars_std(const uint8_t* __restrict__ scalars, uint32_t n, uint8_t* __restrict__ out, ZeroList z) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    z.run(i, gridDim.x * blockDim.x);
     if (i >= n) return;
     store<FrCfg>(out + 32 * (size_t)i, from_mont(load<FrCfg>(scalars + 32 * (size_t)i)));
 }
@@ -621,25 +624,32 @@ size_t digits_src_bytes(uint32_t n, int split) { return (size_t)n * (split == 4 
 
 // the tiled digit kernels' sources: split halves / quarters (sign-magnitude uint4s) or
 // standard-form scalars; nidx = digit-source entries
+__global__ void k_zero_list(ZeroList z) { z.run(blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x); }
+
+// the MSM's first kernel also clears the words later kernels accumulate into (ZeroList): a
+// separate hipMemsetAsync is a fill kernel of its own, ~9-18 us on the critical path each
 static eIcicleError digit_sources(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint8_t* dsrc,
-                                  hipStream_t st, const uint32_t*& src, uint32_t& nidx) {
+                                  const ZeroList& z, hipStream_t st, const uint32_t*& src, uint32_t& nidx) {
     dim3 g((n + 255) / 256);
     if (P.split == 2) {
         if (mont)
-            hipLaunchKernelGGL(k_glv_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+            hipLaunchKernelGGL(k_glv_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);
         else
-            hipLaunchKernelGGL(k_glv_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+            hipLaunchKernelGGL(k_glv_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);
         src = (const uint32_t*)dsrc;
         nidx = 2 * n;
     } else if (P.split == 4) {
         if (mont)
-            hipLaunchKernelGGL(k_psi_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+            hipLaunchKernelGGL(k_psi_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);
         else
-            hipLaunchKernelGGL(k_psi_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc);
+            hipLaunchKernelGGL(k_psi_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);
         src = (const uint32_t*)dsrc;
         nidx = 4 * n;
     } else {
-        if (mont) hipLaunchKernelGGL(k_scalars_std, g, dim3(256), 0, st, scalars, n, dsrc);
+        if (mont)
+            hipLaunchKernelGGL(k_scalars_std, g, dim3(256), 0, st, scalars, n, dsrc, z);
+        else
+            hipLaunchKernelGGL(k_zero_list, dim3(8), dim3(256), 0, st, z);
         src = (const uint32_t*)(mont ? dsrc : scalars);
         nidx = n;
     }
@@ -653,7 +663,7 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
     if (P.B <= DT_MAX_B) {
         const uint32_t* src;
         uint32_t nidx;
-        eIcicleError er = digit_sources(scalars, mont, n, P, dsrc, st, src, nidx);
+        eIcicleError er = digit_sources(scalars, mont, n, P, dsrc, ZeroList{}, st, src, nidx);
         if (er != MBLS_SUCCESS) return er;
         const uint32_t tiles = (nidx + DT_TILE - 1) / DT_TILE;
         dim3 gt(tiles * (uint32_t)P.W);
@@ -911,7 +921,7 @@ static constexpr uint32_t PS_TEAM = MBLS_PS_TEAM;
 template <bool PACK>
 __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ ent, const uint32_t* __restrict__ seg_off,
                                                    const uint32_t* __restrict__ seg_cnt,
-                                                   const uint32_t* __restrict__ part_base, uint32_t tiles, int W,
+                                                   const uint32_t* __restrict__ part_tot, uint32_t tiles, int W,
                                                    int Wg, uint32_t B, int FB, uint32_t NP,
                                                    uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets,
                                                    uint32_t* __restrict__ sorted) {
@@ -933,8 +943,20 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
             atomicAdd(&cnt[fine], 1u);
         }
     }
+    // this part's base: the sum of the part totals before it (blockIdx = wl * NP + part, the
+    // scan order); block 0 sums them all for offsets[Wg B].  <= Wg * NP = 2048 words: cheaper
+    // than the three launches of a separate scan
+    __shared__ uint32_t wsum[4];
+    {
+        const uint32_t lim = blockIdx.x == 0 ? (uint32_t)Wg * NP : blockIdx.x;
+        uint32_t a = 0;
+        for (uint32_t k = threadIdx.x; k < lim; k += blockDim.x) a += part_tot[k];
+        for (int d = 32; d > 0; d >>= 1) a += __shfl_xor(a, d, 64);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = a;
+    }
     __syncthreads();
-    const uint32_t base = part_base[wl * NP + part];
+    const uint32_t psum = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    const uint32_t base = blockIdx.x == 0 ? 0u : psum;
     if (threadIdx.x < 64) {  // wave 0: exclusive scan of the FBN <= 128 fine counts, 2 per lane
         const uint32_t l = threadIdx.x;
         const uint32_t h0 = 2 * l < FBN ? cnt[2 * l] : 0u, h1 = 2 * l + 1 < FBN ? cnt[2 * l + 1] : 0u;
@@ -951,7 +973,7 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
             offsets[key + 1] = base + run + h0;
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 64) offsets[(size_t)Wg * B] = part_base[(size_t)Wg * NP];
+    if (blockIdx.x == 0 && threadIdx.x == 64) offsets[(size_t)Wg * B] = psum;
     __syncthreads();
     if (threadIdx.x < FBN) cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -969,14 +991,18 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
 
 eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* ent,
                                 uint32_t* seg_off, uint32_t* seg_cnt, uint32_t* part_tot, uint8_t* dsrc,
-                                hipStream_t st) {
+                                uint32_t* zero_word, hipStream_t st) {
     if (P.B > DT_MAX_B) return MBLS_INVALID_ARGUMENT;
     const PartSortSizes z = part_sort_sizes(P);
     const uint32_t* src;
     uint32_t nidx;
-    eIcicleError er = digit_sources(scalars, mont, n, P, dsrc, st, src, nidx);
+    ZeroList zl;
+    zl.p[0] = part_tot;  // k_digits_part's per-part totals (atomics)
+    zl.n[0] = (uint32_t)P.Wg * z.NP;
+    zl.p[1] = zero_word;  // the chunk-count maximum (k_chunk_counts' atomicMax)
+    zl.n[1] = zero_word ? 1u : 0u;
+    eIcicleError er = digit_sources(scalars, mont, n, P, dsrc, zl, st, src, nidx);
     if (er != MBLS_SUCCESS) return er;
-    MBLS_TRY(hipMemsetAsync(part_tot, 0, (size_t)P.Wg * z.NP * 4, st));
     dim3 g(z.segments), b(DT_THREADS);
     const uint32_t F = (uint32_t)P.F;
 #define MBLS_DP(S_, P_)                                                                                           \
@@ -1000,14 +1026,14 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
                               const uint32_t* part_tot, uint32_t* part_base, uint32_t* tmp, uint32_t* counts,
                               uint32_t* offsets, uint32_t* sorted, hipStream_t st) {
     const PartSortSizes z = part_sort_sizes(P);
-    eIcicleError er = scan_exclusive(part_tot, part_base, (uint32_t)P.Wg * z.NP, tmp, st);
-    if (er != MBLS_SUCCESS) return er;
+    (void)part_base;
+    (void)tmp;
     dim3 g((uint32_t)P.Wg * z.NP), b(256);
     if (z.pack)
-        hipLaunchKernelGGL(k_part_sort<true>, g, b, 0, st, ent, seg_off, seg_cnt, part_base, z.tiles, P.W, P.Wg, P.B,
+        hipLaunchKernelGGL(k_part_sort<true>, g, b, 0, st, ent, seg_off, seg_cnt, part_tot, z.tiles, P.W, P.Wg, P.B,
                            z.FB, z.NP, counts, offsets, sorted);
     else
-        hipLaunchKernelGGL(k_part_sort<false>, g, b, 0, st, ent, seg_off, seg_cnt, part_base, z.tiles, P.W, P.Wg, P.B,
+        hipLaunchKernelGGL(k_part_sort<false>, g, b, 0, st, ent, seg_off, seg_cnt, part_tot, z.tiles, P.W, P.Wg, P.B,
                            z.FB, z.NP, counts, offsets, sorted);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
@@ -1051,24 +1077,14 @@ __global__ void k_chunk_counts(const uint32_t* __restrict__ counts, const uint32
     if (threadIdx.x < ORDER_BINS) binhist[order_index(blockIdx.x, threadIdx.x, bpg)] = hist[threadIdx.x];
 }
 
-// perm = the light buckets (<= SMALL_MAX chunks) grouped by window group, then by chunk count
-// (heaviest first), so the waves of k_bucket_small run uniform trip counts (bucket order alone
-// gave ~4 +- 1.5 chunks per lane and a wave ran its maximum).  binbase = exclusive scan of
-// k_chunk_counts' histograms (order_index layout).
-__global__ void k_bucket_order(const uint32_t* __restrict__ nchunks, uint32_t m, const uint32_t* __restrict__ binbase,
-                               uint32_t bpg, uint32_t* __restrict__ perm) {
-    __shared__ uint32_t cur[ORDER_BINS];
-    if (threadIdx.x < ORDER_BINS) cur[threadIdx.x] = binbase[order_index(blockIdx.x, threadIdx.x, bpg)];
-    __syncthreads();
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= m) return;
-    const uint32_t c = nchunks[b];
-    if (c <= SMALL_MAX) perm[atomicAdd(&cur[c], 1u)] = b;
-}
+// perm (k_chunk_owner) = the light buckets (<= SMALL_MAX chunks) grouped by window group, then
+// by chunk count (heaviest first), so the waves of k_bucket_small run uniform trip counts (bucket
+// order alone gave ~4 +- 1.5 chunks per lane and a wave ran its maximum).  binbase = exclusive
+// scan of k_chunk_counts' histograms (order_index layout).
 
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
-                                 uint32_t L, uint32_t* binhist, uint32_t groups, hipStream_t st) {
-    MBLS_TRY(hipMemsetAsync(nchunks + m, 0, 4, st));
+                                 uint32_t L, uint32_t* binhist, uint32_t groups, bool zeroed, hipStream_t st) {
+    if (!zeroed) MBLS_TRY(hipMemsetAsync(nchunks + m, 0, 4, st));
     const uint32_t nblk = (m + 255) / 256;
     hipLaunchKernelGGL(k_chunk_counts, dim3(nblk), dim3(256), 0, st, counts, offsets, nchunks, m, L, binhist,
                        nblk / groups);
@@ -1078,12 +1094,36 @@ eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets
 
 uint32_t order_words(uint32_t m) { return ORDER_BINS * ((m + 255) / 256); }
 
-eIcicleError launch_bucket_order(const uint32_t* nchunks, uint32_t m, const uint32_t* binhist, uint32_t* binbase,
-                                 uint32_t* tmp, uint32_t* perm, uint32_t groups, hipStream_t st) {
-    eIcicleError er = scan_exclusive(binhist, binbase, order_words(m), tmp, st);
-    if (er != MBLS_SUCCESS) return er;
-    const uint32_t nblk = (m + 255) / 256;
-    hipLaunchKernelGGL(k_bucket_order, dim3(nblk), dim3(256), 0, st, nchunks, m, binbase, nblk / groups, perm);
+// exclusive scan of a short array (the order histograms, ~17 K words) in ONE workgroup; out[m]
+// = total
+__global__ __launch_bounds__(1024) void k_scan_small(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                     uint32_t m) {
+    __shared__ uint32_t wtot[16];
+    const uint32_t per = (m + 1023) / 1024;
+    const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, m);
+    uint32_t a = 0;
+    for (uint32_t k = b0; k < b1; ++k) a += in[k];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = a;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += t;
+    }
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t k = 0; k < w; ++k) wbase += wtot[k];
+    uint32_t run = wbase + incl - a;
+    for (uint32_t k = b0; k < b1; ++k) {
+        const uint32_t v = in[k];
+        out[k] = run;
+        run += v;
+    }
+    if (threadIdx.x == 1023) out[m] = run;
+}
+
+eIcicleError launch_order_scan(const uint32_t* binhist, uint32_t* binbase, uint32_t m, hipStream_t st) {
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, binhist, binbase, order_words(m));
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }
@@ -1109,19 +1149,31 @@ eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const ui
     return MBLS_SUCCESS;
 }
 
-// owner[segment] = bucket; first[t] = the bucket holding position L t (the start of chunk t)
+// owner[segment] = bucket; first[t] = the bucket holding position L t (the start of chunk t);
+// and the bucket order of k_bucket_order (same grid: one thread per bucket)
 __global__ void k_chunk_owner(const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ offsets, uint32_t m,
-                              uint32_t L, uint32_t* __restrict__ owner, uint32_t* __restrict__ first) {
+                              uint32_t L, uint32_t* __restrict__ owner, uint32_t* __restrict__ first,
+                              const uint32_t* __restrict__ nchunks, const uint32_t* __restrict__ binbase, uint32_t bpg,
+                              uint32_t* __restrict__ perm) {
+    __shared__ uint32_t cur[ORDER_BINS];
+    if (threadIdx.x < ORDER_BINS) cur[threadIdx.x] = binbase[order_index(blockIdx.x, threadIdx.x, bpg)];
+    __syncthreads();
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
-    for (uint32_t k = chunk_off[b]; k < chunk_off[b + 1]; ++k) owner[k] = b;
+    const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
+    for (uint32_t k = k0; k < k1; ++k) owner[k] = b;
     const uint32_t o = offsets[b], e = offsets[b + 1];
     for (uint32_t t = (o + L - 1) / L; t * L < e; ++t) first[t] = b;
+    const uint32_t c = nchunks[b];
+    if (c <= SMALL_MAX) perm[atomicAdd(&cur[c], 1u)] = b;
 }
 
 eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offsets, uint32_t m, uint32_t L,
-                                uint32_t* owner, uint32_t* first, hipStream_t st) {
-    hipLaunchKernelGGL(k_chunk_owner, dim3((m + 255) / 256), dim3(256), 0, st, chunk_off, offsets, m, L, owner, first);
+                                uint32_t* owner, uint32_t* first, const uint32_t* nchunks, const uint32_t* binbase,
+                                uint32_t groups, uint32_t* perm, hipStream_t st) {
+    const uint32_t nblk = (m + 255) / 256;
+    hipLaunchKernelGGL(k_chunk_owner, dim3(nblk), dim3(256), 0, st, chunk_off, offsets, m, L, owner, first, nchunks,
+                       binbase, nblk / groups, perm);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }

@@ -69,6 +69,16 @@ static constexpr int MAX_PRECOMPUTE = 64;
 static constexpr int SMALL_MAX = 16;  // buckets of <= SMALL_MAX chunks: one thread (k_bucket_small)
 static constexpr int ORDER_BINS = SMALL_MAX + 1;  // k_bucket_order bins: chunk counts 0..SMALL_MAX
 
+// words a kernel clears in passing (grid-stride), instead of a hipMemsetAsync fill launch
+struct ZeroList {
+    uint32_t* p[2] = {nullptr, nullptr};
+    uint32_t n[2] = {0, 0};
+    MBLS_DEV void run(uint32_t gid, uint32_t stride) const {
+        for (int k = 0; k < 2; ++k)
+            for (uint32_t i = gid; i < n[k]; i += stride) p[k][i] = 0;
+    }
+};
+
 struct MsmPlan {
     int c, W, Wg, F;
     int sF;                     // precomputed-table block shift in bits (0: F == 1), see window_span
@@ -103,14 +113,14 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
 size_t digits_src_bytes(uint32_t n, int split);
 eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint32_t* tmp, hipStream_t st);
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
-                                 uint32_t L, uint32_t* binhist, uint32_t groups, hipStream_t st);
-eIcicleError launch_bucket_order(const uint32_t* nchunks, uint32_t m, const uint32_t* binhist, uint32_t* binbase,
-                                 uint32_t* tmp, uint32_t* perm, uint32_t groups, hipStream_t st);
+                                 uint32_t L, uint32_t* binhist, uint32_t groups, bool zeroed, hipStream_t st);
+eIcicleError launch_order_scan(const uint32_t* binhist, uint32_t* binbase, uint32_t m, hipStream_t st);
 uint32_t order_words(uint32_t m);
 eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const uint32_t* ranks, size_t total,
                             const uint32_t* offsets, uint32_t* sorted, hipStream_t st);
 eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offsets, uint32_t m, uint32_t L,
-                                uint32_t* owner, uint32_t* first, hipStream_t st);
+                                uint32_t* owner, uint32_t* first, const uint32_t* nchunks, const uint32_t* binbase,
+                                uint32_t groups, uint32_t* perm, hipStream_t st);
 eIcicleError launch_scalars_from_mont(uint8_t* s, size_t n, hipStream_t st);
 eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
 eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
@@ -128,7 +138,7 @@ bool partition_sort(const MsmPlan& P);
 PartSortSizes part_sort_sizes(const MsmPlan& P);
 eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* ent,
                                 uint32_t* seg_off, uint32_t* seg_cnt, uint32_t* part_tot, uint8_t* dsrc,
-                                hipStream_t st);
+                                uint32_t* zero_word, hipStream_t st);
 eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint32_t* seg_off, const uint32_t* seg_cnt,
                               const uint32_t* part_tot, uint32_t* part_base, uint32_t* tmp, uint32_t* counts,
                               uint32_t* offsets, uint32_t* sorted, hipStream_t st);
@@ -924,7 +934,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     {
         ProfScope ps("msm.digits", st);
         if (psort) {
-            er = launch_digits_part(scalars, scalars_mont, n, P, ent, seg_off, seg_cnt, part_tot, dsrc, st);
+            er = launch_digits_part(scalars, scalars_mont, n, P, ent, seg_off, seg_cnt, part_tot, dsrc, nchunks + TB, st);
         } else {
             MBLS_TRY(hipMemsetAsync(counts, 0, (size_t)TB * 4, st));
             er = launch_digits(scalars, scalars_mont, n, P, keys, vals, ranks, counts, dsrc, st);
@@ -939,12 +949,14 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         } else if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) {
             return er;
         }
-        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, P.groups, st)) != MBLS_SUCCESS)
+        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, P.groups, psort, st)) != MBLS_SUCCESS)
             return er;
+        if ((er = launch_order_scan(binhist, binbase, TB, st)) != MBLS_SUCCESS) return er;
         if ((er = scan_exclusive(nchunks, chunk_off, TB, tmp, st)) != MBLS_SUCCESS) return er;
         if (!psort && (er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
-        if ((er = launch_chunk_owner(chunk_off, offsets, TB, P.chunk, owner, first, st)) != MBLS_SUCCESS) return er;
-        if ((er = launch_bucket_order(nchunks, TB, binhist, binbase, tmp, perm, P.groups, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_chunk_owner(chunk_off, offsets, TB, P.chunk, owner, first, nchunks, binbase, P.groups, perm, st)) !=
+            MBLS_SUCCESS)
+            return er;
     }
     // worst case: every contribution of a window in one bucket
     const uint32_t max_per_bucket = (uint32_t)((P.pts + P.chunk - 1) / P.chunk);
