@@ -756,20 +756,28 @@ inline AccKernel accumulate_kernel() {
     return k_accumulate<F, 1>;
 }
 
-// contributions per accumulation thread.  Default CHUNK (16): measured against spreading NC over
-// one round of resident waves (MBLS_ACC_CHUNK=auto, 86 at G1 2^20) the longer chunks cut the
-// bucket sums (0.61 -> 0.19 ms) but cost more in the accumulation (3.25 -> 3.66 ms): a chunk's
-// first addition is free when the whole wave starts a chunk together (acc = P, counter-checked:
-// SQ_INSTS_VALU +5.2% at 86), and the rest of the gap is not explained by instruction counts
-// (DESIGN.md section 8).  MBLS_ACC_CHUNK=<n> fixes it (A/B runs).
+// contributions per accumulation thread: CHUNK (16), or an eighth of the average bucket when
+// buckets are bigger (2^24 points: 1024 contributions per bucket, chunk 128), so a bucket keeps
+// <= ~9 partials and its sum stays on the one-thread-per-bucket path (k_bucket_small) -- with
+// 16-point chunks every bucket at 2^24 had 64 partials, took the heavy-bucket tree passes and
+// the bucket sums cost 93.5 ms against 50.6 ms of accumulation.  Short chunks pay off below
+// that: a chunk's first addition is free when the whole wave starts a chunk together (acc = P,
+// counter-checked: SQ_INSTS_VALU +5.2% at 86 instead of 16 at 2^20), and spreading NC over one
+// round of resident waves (MBLS_ACC_CHUNK=auto, 86 at G1 2^20) cut the bucket sums 0.61 ->
+// 0.19 ms but cost 3.25 -> 3.66 ms in the accumulation.
+// MBLS_ACC_CHUNK=<n> fixes it (A/B runs).
 template <class F>
-inline uint32_t accumulate_chunk(size_t NC) {
+inline uint32_t accumulate_chunk(const MsmPlan& P) {
     static const long fixed = [] {
         const char* e = getenv("MBLS_ACC_CHUNK");
-        if (!e) return (long)CHUNK;
+        if (!e) return -1L;
         return strcmp(e, "auto") == 0 ? 0L : atol(e);
     }();
     if (fixed > 0) return (uint32_t)fixed;
+    if (fixed < 0) {
+        const size_t per_bucket = P.contributions / std::max<uint32_t>(P.TB, 1u);
+        return (uint32_t)std::max<size_t>(CHUNK, per_bucket / 8);
+    }
     static const size_t resident = [] {
         int dev = 0, cus = 0, blocks = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -781,7 +789,7 @@ inline uint32_t accumulate_chunk(size_t NC) {
         return (size_t)cus * blocks * 256 / LaneOf<F>::LANES;  // chains resident at once
     }();
     if (!resident) return CHUNK;
-    const size_t L = (NC + resident - 1) / resident;
+    const size_t L = (P.contributions + resident - 1) / resident;
     return (uint32_t)std::max<size_t>(CHUNK, L);
 }
 
@@ -1145,7 +1153,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     size_t st_s = (!cfg->are_scalars_on_device) ? align_up(n * 32 * batch) : 0;
     size_t st_b = (!cfg->are_points_on_device || !pts_mont) ? align_up(nbases * AFF) : 0;
     size_t st_r = align_up(JAC * (size_t)batch);
-    P.chunk = accumulate_chunk<F>(P.contributions);
+    P.chunk = accumulate_chunk<F>(P);
     // window groups pipeline one MSM's tails behind its own accumulations (side streams); the
     // pipelined batch members already overlap each other's tails and run without side streams
     er = set_groups(P, batch >= 2 && batch_pipeline() ? 1 : msm_groups());
