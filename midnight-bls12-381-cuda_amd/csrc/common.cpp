@@ -109,6 +109,8 @@ eIcicleError StreamCtx::ensure_pipe() {
         if (!pipe[k]) MBLS_TRY(hipStreamCreateWithFlags(&pipe[k], hipStreamNonBlocking));
     for (int k = 0; k < 3; ++k)
         if (!pipe_ev[k]) MBLS_TRY(hipEventCreateWithFlags(&pipe_ev[k], hipEventDisableTiming));
+    for (int k = 0; k < 2; ++k)
+        if (!acc_ev[k]) MBLS_TRY(hipEventCreateWithFlags(&acc_ev[k], hipEventDisableTiming));
     return MBLS_SUCCESS;
 }
 

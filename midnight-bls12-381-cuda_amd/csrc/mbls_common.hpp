@@ -60,6 +60,9 @@ struct StreamCtx {
     // accumulation; pipe_ev[0] forks them from this stream, pipe_ev[1..2] join them back
     hipStream_t pipe[2] = {nullptr, nullptr};
     hipEvent_t pipe_ev[3] = {nullptr, nullptr, nullptr};
+    // acc_ev[b & 1]: member b's accumulation done; member b + 1 (other stream) waits for it, so
+    // the two streams run staggered (b+1 accumulates while b runs its tail) instead of lockstep
+    hipEvent_t acc_ev[2] = {nullptr, nullptr};
     explicit StreamCtx(hipStream_t s) : arena(s) {}
     eIcicleError ensure_side(size_t nevents, size_t nsides = 1);
     eIcicleError ensure_pipe();
