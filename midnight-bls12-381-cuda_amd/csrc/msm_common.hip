@@ -35,6 +35,7 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     //   G2 psi: four quarter-width streams, |m| < 2^63 (tiled digits only, c <= 16; worth it
     //   only for wide scalars: plain needs ceil((bits+1)/c) windows of n, psi 4 x ceil(64/c)).
     p.split = 1;
+    p.fq2 = endo == 4;
     if (endo == 2 && F == 1 && bits > 128) p.split = 2;
     if (endo == 4 && F == 1 && bits > 192 && c <= 16) p.split = 4;
     if (F > MAX_PRECOMPUTE) return MBLS_INVALID_ARGUMENT;
@@ -96,7 +97,7 @@ eIcicleError plan_levels(MsmPlan& p, int Wl) {
         const uint32_t lane_chains = ((m + (1u << SEG0_LOG) - 1) >> SEG0_LOG) * (uint32_t)Wl;
         if (p.levels > 0 || lane_chains < lane_min) {
             const uint32_t row_chains = ((m + (1u << row_log) - 1) >> row_log) * (uint32_t)Wl;
-            mode = row_chains >= wave_min_chains() ? MODE_ROW : MODE_WAVE;
+            mode = row_chains >= wave_min_chains(p.fq2) ? MODE_ROW : MODE_WAVE;
             lg = mode == MODE_ROW ? row_log : wave_log;
         }
         p.seg_log[p.levels] = (uint8_t)lg;

@@ -83,6 +83,7 @@ struct MsmPlan {
     int c, W, Wg, F;
     int sF;                     // precomputed-table block shift in bits (0: F == 1), see window_span
     int split;                  // endomorphism split: 1 none, 2 G1 GLV (phi), 4 G2 psi
+    bool fq2;                   // G2 (Fq2 coordinates)
     uint32_t B, TB;
     uint32_t chunk;             // contributions per accumulation thread (accumulate_chunk)
     size_t pts;                 // distinct point indices (n, n*F, or split*n)
@@ -686,13 +687,20 @@ inline bool batch_pipeline() {
     return v;
 }
 
-// reduction levels with fewer segments than this run one segment per wave (MBLS_WAVE_MIN tunes)
-inline uint32_t wave_min_chains() {
+// reduction levels with fewer segments than this run one segment per wave (MBLS_WAVE_MIN tunes;
+// G2: MBLS_WAVE_MIN_G2).  An Fq2 row-sliced addition is three row products per Fq2 product in
+// series, so G2 switches to the wave layout (the three spread over rows) at more segments:
+// G2 2^20 level 1 (2048 segments of 16) 0.81 ms in rows.
+inline uint32_t wave_min_chains(bool fq2 = false) {
     static const uint32_t v = [] {
         const char* e = getenv("MBLS_WAVE_MIN");
         return e ? (uint32_t)atoi(e) : 2048u;
     }();
-    return v;
+    static const uint32_t v2 = [] {
+        const char* e = getenv("MBLS_WAVE_MIN_G2");
+        return e ? (uint32_t)atoi(e) : 8192u;
+    }();
+    return fq2 ? v2 : v;
 }
 inline uint32_t tree_blocks(uint32_t m) { return (m + 16 * TREE_PER_ROW - 1) / (16 * TREE_PER_ROW); }
 
