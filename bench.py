@@ -59,6 +59,27 @@ def pmc_traffic(kernel):
     return None if not k or k.get("hbm_bytes_per_launch") is None else k["hbm_bytes_per_launch"]
 
 
+def pmc_counter(kernel, counter):
+    d, _ = pmc_summary()
+    return d.get("kernels", {}).get(kernel, {}).get(counter)
+
+
+# VALU issue cost in cycles per wave-instruction: v_mad_u64_u32 (an INT64 instruction) is
+# quarter rate, 8 cycles (profiles/r01/microbench.txt: 34.3 mad/clk/CU); other VALU 2 cycles
+# (MI355X_MICROARCH.md: a wave issues a VALU instruction over 2 cycles)
+MAD_CYCLES, VALU_CYCLES, SIMDS, CLOCK_GHZ = 8, 2, 1024, 2.4
+
+
+def valu_issue_bound_ms(kernel):
+    """lower bound on a kernel's duration from its committed VALU instruction counts: every
+    INT64 instruction at the mad cost, the rest at the full rate, all SIMDs busy"""
+    v, i64 = pmc_counter(kernel, "SQ_INSTS_VALU"), pmc_counter(kernel, "SQ_INSTS_VALU_INT64")
+    if v is None or i64 is None:
+        return None
+    cycles = (i64 * MAD_CYCLES + (v - i64) * VALU_CYCLES) / SIMDS
+    return cycles / (CLOCK_GHZ * 1e6)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -250,6 +271,9 @@ def main():
         ntt_ach = NTT_BYTES_PER_ELEM * nn / (ntt_ms * 1e-3) / 1e9 if ntt_ms else None
         ntt_mad_t = (nn // 2) * args.ntt_log * MADS_PER_FR_MUL / (ntt_ms * 1e-3) / 1e12 if ntt_ms else None
         _, pmc_src = pmc_summary()
+        passes = [valu_issue_bound_ms(k) for k in ("k_ntt_pass<true, false, false>", "k_ntt_pass<false, false, false>",
+                                                     "k_ntt_pass<false, true, false>")]
+        ntt_issue_ms = round(sum(passes), 4) if args.ntt_log == 22 and all(p is not None for p in passes) else None
         out = {
             "metric": "G1 MSM/sec at 2^20 points + Fr NTT/sec at 2^22 (bit-exact vs BLST)",
             "value": round(msm_per_sec, 3),
@@ -282,9 +306,18 @@ def main():
                               "achieved": round(mad_t, 3) if mad_t else None, "peak": MAD_RATE_T,
                               "unit": "T v_mad_u64_u32/s", "frac": round(mad_t / MAD_RATE_T, 4) if mad_t else None,
                               "mads_per_launch": contributions * MADS_PER_G1_MADD,
+                              "counter_int64_per_launch": (round(i64 * 64) if (i64 := pmc_counter("k_accumulate", "SQ_INSTS_VALU_INT64")) else None),
+                              "counter_valu_insts_per_launch": pmc_counter("k_accumulate", "SQ_INSTS_VALU"),
+                              "counter_issue_bound_ms": (round(b, 4) if (b := valu_issue_bound_ms("k_accumulate")) else None),
+                              "counter_issue_frac": (round(b / acc_ms, 4) if (b := valu_issue_bound_ms("k_accumulate")) and acc_ms else None),
+                              "counter_source": f"{pmc_src} (SQ_INSTS_VALU, SQ_INSTS_VALU_INT64 per launch)" if pmc_src else None,
                               "note": f"{contributions} mixed additions x {MADS_PER_G1_MADD} mads "
-                                      "(algorithmic); peak = measured mad issue rate"},
+                                      "(algorithmic); peak = measured mad issue rate; counter_issue_frac = the "
+                                      "kernel's VALU issue time from its committed instruction counts (INT64 at 8, "
+                                      "other VALU at 2 cycles per wave-instruction, 1024 SIMDs, 2.4 GHz) / its "
+                                      "measured time"},
             "roofline_ntt": {"kernel": "k_ntt_pass x passes (one transform)", "bound": "hbm",
+                             "counter_issue_bound_ms": ntt_issue_ms, "counter_issue_frac": (round(ntt_issue_ms / ntt_ms, 4) if ntt_issue_ms and ntt_ms else None),
                              "achieved": round(ntt_ach, 2) if ntt_ach else None, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(ntt_ach / HBM_PEAK_GBS, 5) if ntt_ach else None,
                              "traffic": ntt_traffic(args.ntt_log),

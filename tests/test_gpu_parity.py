@@ -578,6 +578,25 @@ def test_bench_ntt_2_22_single_and_batch4(amd):
     assert torch.equal(z, x)
 
 
+@pytest.mark.parametrize("log_n", [21, 22])
+def test_msm_g1_chunk_scaling_sizes(amd, gh, log_n):
+    """the accumulation chunk scales with the bucket size (16 at 2^21, 32 at 2^22, 128 at 2^24:
+    msm_core.hpp accumulate_chunk); 2^21 / 2^22 G1 MSMs through the ICICLE entry equal the
+    oracle (2^24 is test_msm_g1_2_24_single_and_sharded)"""
+    import torch
+    n = 1 << log_n
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0006, montgomery=True)
+    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 0x5EED0016)
+    out = torch.zeros((1, 18), dtype=torch.int64, device="cuda")
+    amd.msm("g1", s, b, scalars_mont=True, out=out)
+    torch.cuda.synchronize()
+    got = gh.decode_icicle("g1", amd.to_numpy_u64(out)[0])
+    ref = H.oracle_msm("g1", _oracle_std_scalars(0x5EED0006, n), amd.to_numpy_u64(b), threads=ORACLE_THREADS)
+    assert got == H.g1_from_affine_mont(ref)
+
+
 @pytest.mark.slow
 def test_msm_g1_2_24_single_and_sharded(amd, gh):
     """north-star size (BASELINE config #4): G1 MSM of 2^24 points (scalars 0x5EED0004, bases
