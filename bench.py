@@ -114,10 +114,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a one-GPU box (never the driver's runs):
+    # MBLS_BENCH_SAME_DEVICE=1 puts every rank on GPU 0, MBLS_BENCH_BACKEND=gloo replaces RCCL
+    # (which refuses two ranks on one device); the digests must match the N = 1 run
+    if os.environ.get("MBLS_BENCH_SAME_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("MBLS_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     amd.lib()
     stream = torch.cuda.current_stream(dev)
 
@@ -366,8 +375,8 @@ def msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_ov
                                                     out=rb, stream=stream, is_async=True, n=n), breps))
         out["msm_batch"] = {"batch": B, "reps": breps, "ms_per_batch": round(b_ms, 3),
                             "msm_per_sec": round(world * B * 1e3 / b_ms, 3),
-                            "note": "ICICLE batch_size (core/msm.rs msm_batch_with_device_bases), members "
-                                    "pipelined on two HIP streams"}
+                            "note": "ICICLE batch_size (core/msm.rs msm_batch_with_device_bases), members in "
+                                    "order on the caller's stream, one (x,y,1) normalisation launch for the batch"}
         del sb
     return out
 

@@ -24,6 +24,12 @@ def gather_partials(partial, world, dist, out=None):
         return partial.reshape(1, -1)
     if out is None:
         out = torch.empty((world, partial.numel()), dtype=partial.dtype, device=partial.device)
+    if partial.is_cuda and dist.get_backend() != "nccl":
+        # gloo (CPU tests, one-GPU rehearsals): stage through host memory
+        host = torch.empty((world, partial.numel()), dtype=partial.dtype)
+        dist.all_gather_into_tensor(host, partial.reshape(1, -1).cpu())
+        out.copy_(host)
+        return out
     dist.all_gather_into_tensor(out, partial.reshape(1, -1).contiguous())
     return out
 
