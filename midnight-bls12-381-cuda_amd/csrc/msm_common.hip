@@ -465,6 +465,9 @@ __global__ __launch_bounds__(256) void k_psi_split(const uint8_t* __restrict__ s
 
 // psi(x, y) = (conj(x) * CX, conj(y) * CY), CX = (0, CX1) (oracle/pyref.py PSI_CX / PSI_CY),
 // Montgomery limbs; the table holds psi^1..3(P_i) at (j-1)*n + i
+// psi^2 x-multiplier C2 = 0x1a0111ea...00000000aaac (an Fq cube root of unity), Montgomery form
+__constant__ uint32_t PSI2_CX_MONT[12] = {0x8671f071u, 0xcd03c9e4u, 0x1fcda5d2u, 0x5dab2246u, 0xd3851b95u, 0x587042afu,
+                                          0x01bacb9eu, 0x8eb60ebeu, 0x83d050d2u, 0x03f97d6eu, 0x54638741u, 0x18f02065u};
 __constant__ uint32_t PSI_CX1_MONT[12] = {0x867545c3u, 0x890dc9e4u, 0x3285a5d5u, 0x2af32253u, 0x309b7e2cu, 0x50880866u,
                                           0x7e881024u, 0xa20d1b8cu, 0xe2db9068u, 0x14e4f04fu, 0x1564853au, 0x14e56d3fu};
 __constant__ uint32_t PSI_CY0_MONT[12] = {0xa55c9ad1u, 0x3e2f585du, 0x86c18183u, 0x4294213du, 0x8b623732u, 0x382844c8u,
@@ -472,7 +475,7 @@ __constant__ uint32_t PSI_CY0_MONT[12] = {0xa55c9ad1u, 0x3e2f585du, 0x86c18183u,
 __constant__ uint32_t PSI_CY1_MONT[12] = {0x5aa30fdau, 0x7bcfa7a2u, 0x2a927e7cu, 0xdc17dec1u, 0x6b4ebef1u, 0x2f088dd8u,
                                           0xda74d4a7u, 0xd1ca2087u, 0x96cebc1du, 0x2da25966u, 0xbbfd87d2u, 0x0e2b7eedu};
 
-__global__ void k_psi_table(const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi, uint32_t n) {
+__global__ __launch_bounds__(256) void k_psi_table(const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi, uint32_t n) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Fq cx1;
@@ -483,16 +486,25 @@ __global__ void k_psi_table(const uint8_t* __restrict__ bases, uint8_t* __restri
         cy.c0.v[k] = PSI_CY0_MONT[k];
         cy.c1.v[k] = PSI_CY1_MONT[k];
     }
-    Affine<Fq2> p = load_affine<Fq2>(bases, i);
-    for (int j = 0; j < 3; ++j) {
-        // conj(x) * (CX1 u) = x1 CX1 + x0 CX1 u; identity (0, 0) maps to itself
-        Affine<Fq2> q;
-        q.x.c0 = p.x.c1 * cx1;
-        q.x.c1 = p.x.c0 * cx1;
-        q.y = Fq2{p.y.c0, neg(p.y.c1)} * cy;
-        p = q;
-        store_affine<Fq2>(phi, (size_t)j * n + i, p);
+    const Affine<Fq2> p = load_affine<Fq2>(bases, i);
+    // psi(P): conj(x) * (CX1 u) = x1 CX1 + x0 CX1 u, conj(y) * CY (5 Fq products); identity
+    // (0, 0) maps to itself
+    Affine<Fq2> q1;
+    q1.x.c0 = p.x.c1 * cx1;
+    q1.x.c1 = p.x.c0 * cx1;
+    {  // conj(y) * CY, Karatsuba in line (fq2_mul is out of line: a call frame in scratch)
+        const Fq a0 = p.y.c0, a1 = neg(p.y.c1);
+        const Fq t0 = a0 * cy.c0, t1 = a1 * cy.c1, t2 = (a0 + a1) * (cy.c0 + cy.c1);
+        q1.y = Fq2{t0 - t1, (t2 - t0) - t1};
     }
+    store_affine<Fq2>(phi, i, q1);
+    // psi^2 = (x, y) -> (C2 x, -y) with C2 in Fq (oracle/pyref.py psi, checked numerically),
+    // so psi^2(P) and psi^3(P) = psi^2(psi(P)) take 2 Fq products each (15 -> 9 per point)
+    Fq c2;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) c2.v[k] = PSI2_CX_MONT[k];
+    store_affine<Fq2>(phi, (size_t)n + i, Affine<Fq2>{Fq2{p.x.c0 * c2, p.x.c1 * c2}, neg(p.y)});
+    store_affine<Fq2>(phi, 2 * (size_t)n + i, Affine<Fq2>{Fq2{q1.x.c0 * c2, q1.x.c1 * c2}, neg(q1.y)});
 }
 
 eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st) {
@@ -817,12 +829,50 @@ PartSortSizes part_sort_sizes(const MsmPlan& P) {
     return s;
 }
 
+// Signed digits of uniform windows (sF == 0) in closed form: with C = sum_w (B - 1) 2^(c w), the
+// base-2^c digits e_w of s + C give d_w = e_w - (B - 1) in [1 - B, B] -- the unique signed
+// representation with that digit range, so exactly digit_at's carry-chain digits, without its
+// loop over the lower windows (O(w) per digit).  s + C < 2^(c W) for the window counts
+// make_plan picks (no final carry); NW + 1 words hold it.
+struct DigitOffset {
+    uint32_t w[9];
+};
+static DigitOffset digit_offset(int c, int W, uint32_t B) {
+    DigitOffset o{};
+    for (int j = 0; j < W; ++j) {
+        const int pos = c * j;
+        const uint64_t v = (uint64_t)(B - 1) << (pos & 31);
+        const int k = pos >> 5;
+        if (k < 9) o.w[k] += (uint32_t)v;  // windows do not overlap: no carries between terms
+        if (k + 1 < 9) o.w[k + 1] += (uint32_t)(v >> 32);
+    }
+    return o;
+}
+template <int NW>
+MBLS_DEV uint32_t digit_closed(const uint32_t (&x)[NW], const DigitOffset& C, int w, int c, uint32_t B) {
+    uint32_t y[NW + 1];
+    unsigned carry = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) y[k] = __builtin_addc(x[k], C.w[k], carry, &carry);
+    y[NW] = C.w[NW] + carry;
+    const int bit = c * w, word = bit >> 5, sh = bit & 31;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k <= NW; ++k) {
+        lo = (k == word) ? y[k] : lo;
+        hi = (k == word + 1) ? y[k] : hi;
+    }
+    const uint32_t e = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & ((1u << c) - 1);
+    // d = e - (B - 1): positive (e >= B - 1) or -(B - 1 - e), as magnitude | sign bit
+    return e >= B - 1 ? e - (B - 1) : ((B - 1 - e) | 0x80000000u);
+}
+
 template <bool SPLIT, bool PACK>
 __global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __restrict__ src, uint32_t nidx, int c,
                                                             int Wg, int sF, uint32_t F, uint32_t B, int FB, uint32_t NP,
                                                             uint32_t* __restrict__ ent, uint32_t* __restrict__ seg_off,
                                                             uint32_t* __restrict__ seg_cnt,
-                                                            uint32_t* __restrict__ part_tot) {
+                                                            uint32_t* __restrict__ part_tot, DigitOffset C) {
     __shared__ uint32_t hist[256];
     constexpr int NW = SPLIT ? 4 : 8;
     const uint32_t tiles = (nidx + DT_TILE - 1) / DT_TILE;
@@ -854,7 +904,7 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __re
                 negh = x[3] >> 31;
                 x[3] &= 0x7fffffffu;
             }
-            const uint32_t d = digit_at<NW>(x, w, c, B, Wg, sF) ^ (negh << 31);
+            const uint32_t d = (sF == 0 ? digit_closed<NW>(x, C, w, c, B) : digit_at<NW>(x, w, c, B, Wg, sF)) ^ (negh << 31);
             dig[k] = d;
             if (d & 0x7fffffffu) lr[k] = atomicAdd(&hist[((d & 0x7fffffffu) - 1) >> FB], 1u);
         }
@@ -1006,9 +1056,10 @@ eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, c
     if (er != MBLS_SUCCESS) return er;
     dim3 g(z.segments), b(DT_THREADS);
     const uint32_t F = (uint32_t)P.F;
+    const DigitOffset C = digit_offset(P.c, P.W, P.B);
 #define MBLS_DP(S_, P_)                                                                                           \
     hipLaunchKernelGGL((k_digits_part<S_, P_>), g, b, 0, st, src, nidx, P.c, P.Wg, P.sF, F, P.B, z.FB, z.NP, ent, seg_off, \
-                       seg_cnt, part_tot)
+                       seg_cnt, part_tot, C)
     if (P.split > 1) {
         if (z.pack)
             MBLS_DP(true, true);

@@ -944,11 +944,18 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     hipStream_t side = use_side ? ctx.sides[0] : st;
     hipEvent_t* ev = ctx.events.data() + P.levels + 1;
     if (P.split > 1) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
+        // the psi table (15 Fq products per point) on the main stream before the digit pass
+        // when MBLS_PSI_SERIAL=1 (beside it, the two slow each other)
+        static const bool psi_serial = [] {
+            const char* e = getenv("MBLS_PSI_SERIAL");
+            return e && atoi(e) != 0;
+        }();
+        hipStream_t ts = (P.split == 4 && psi_serial) ? st : side;
         MBLS_TRY(hipEventRecord(ev[0], st));
-        MBLS_TRY(hipStreamWaitEvent(side, ev[0], 0));
-        er = P.split == 2 ? launch_glv_table(bases, phi, n, side) : launch_psi_table(bases, phi, n, side);
+        MBLS_TRY(hipStreamWaitEvent(ts, ev[0], 0));
+        er = P.split == 2 ? launch_glv_table(bases, phi, n, ts) : launch_psi_table(bases, phi, n, ts);
         if (er != MBLS_SUCCESS) return er;
-        MBLS_TRY(hipEventRecord(ev[1], side));
+        MBLS_TRY(hipEventRecord(ev[1], ts));
     }
     {
         ProfScope ps("msm.digits", st);
