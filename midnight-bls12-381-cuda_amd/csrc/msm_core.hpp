@@ -557,8 +557,10 @@ MBLS_DEV RFq2 one_std<RFq2>() {
 
 // one lane per point: the inversion is the binary extended Euclid of mbls_field.hpp (word
 // shifts and adds at the full VALU rate; the row-sliced Fermat chain it replaces took 0.29 ms)
+// (launched with 64 threads: the bound lets the inversion keep its words in VGPRs -- at the
+// default 1024-thread bound it spilled 204 B (G1) / 912 B (G2) to scratch)
 template <class F>
-__global__ void k_jac_to_icicle(uint8_t* pts, int count) {
+__global__ __launch_bounds__(64) void k_jac_to_icicle(uint8_t* pts, int count) {
     const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (i >= count) return;
     Jacobian<F> p = load_jac<F>(pts, i);
@@ -628,7 +630,7 @@ __global__ void k_gen_bases(uint8_t* out, uint64_t seed, size_t start, size_t n)
 // precomputed bases, point-major as ICICLE / core/msm.rs:164-165 document:
 // out[i*factor + f] = 2^(shift*f) * P_i (Montgomery affine)
 template <class F>
-__global__ void k_precompute(const uint8_t* in, uint8_t* out, size_t n, int factor, int shift) {
+__global__ __launch_bounds__(128) void k_precompute(const uint8_t* in, uint8_t* out, size_t n, int factor, int shift) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     Affine<F> a = load_affine<F>(in, i);
@@ -679,12 +681,9 @@ inline bool defer_narrow_trees() {
 // (MBLS_BATCH_PIPE=1: member b+1 accumulates while member b runs its tail).  Measured G1 2^20
 // batch 8: in order 207 MSM/s, staggered pipeline 204 (the tails' row-sliced chains slow the
 // VALU-saturated accumulation beside them about as much as they hide), unstaggered 197
-inline bool batch_pipeline() {
-    static const bool v = [] {
-        const char* e = getenv("MBLS_BATCH_PIPE");
-        return e ? atoi(e) != 0 : false;
-    }();
-    return v;
+inline bool batch_pipeline() {  // read per call: the GPU tests switch it
+    const char* e = getenv("MBLS_BATCH_PIPE");
+    return e ? atoi(e) != 0 : false;
 }
 
 // reduction levels with fewer segments than this run one segment per wave (MBLS_WAVE_MIN tunes;
@@ -871,12 +870,9 @@ eIcicleError reduce_windows(const MsmPlan& P, const uint8_t* V, int Wl, int g, u
 // pass -- the tails are latency-bound row / wave-sliced chains that cost ~4x the VALU issue per
 // product of the lane-sliced accumulation, so beside it they slow the accumulation (3.27 ->
 // 4.15 ms summed over 4 groups) more than they hide.
-inline int msm_groups() {
-    static const int v = [] {
-        const char* e = getenv("MBLS_GROUPS");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
+inline int msm_groups() {  // read per call: the GPU tests switch it
+    const char* e = getenv("MBLS_GROUPS");
+    return e ? atoi(e) : 1;
 }
 
 // Core MSM on device operands: scalars (standard or Montgomery), bases Montgomery affine

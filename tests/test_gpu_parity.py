@@ -578,6 +578,41 @@ def test_bench_ntt_2_22_single_and_batch4(amd):
     assert torch.equal(z, x)
 
 
+@pytest.mark.parametrize("env", [{"MBLS_GROUPS": "2"}, {"MBLS_GROUPS": "4"}, {"MBLS_GROUPS": "8"},
+                                 {"MBLS_BATCH_PIPE": "1"}])
+def test_msm_optional_schedules(amd, gh, env):
+    """the non-default schedules (msm_core.hpp): window groups pipelined over side streams
+    (MBLS_GROUPS) and the staggered two-stream batch pipeline (MBLS_BATCH_PIPE) give the oracle's
+    sums -- G1 with c = 16 (8 GLV windows: groups of 4 / 2 / 1), G2 (4 psi windows), batch of 3"""
+    import os
+    import torch
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        for group, n, w in (("g1", 3000, 12), ("g2", 700, 24)):
+            s = torch.zeros((3 * n, 4), dtype=torch.int64, device="cuda")
+            amd.gen_scalars(s, 0x5EED00D1, montgomery=True)
+            b = torch.zeros((n, w), dtype=torch.int64, device="cuda")
+            amd.gen_bases(group, b, 0x5EED00D2)
+            out = torch.zeros((3, w * 3 // 2), dtype=torch.int64, device="cuda")
+            amd.msm(group, s, b, scalars_mont=True, c=16, batch=3, out=out, n=n)
+            torch.cuda.synchronize()
+            dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
+            for k in range(3):
+                ref = H.oracle_msm(group, _oracle_std_scalars(0x5EED00D1, n, start=k * n), amd.to_numpy_u64(b))
+                assert gh.decode_icicle(group, amd.to_numpy_u64(out)[k]) == dec(ref), (group, k)
+            one = torch.zeros((1, w * 3 // 2), dtype=torch.int64, device="cuda")
+            amd.msm(group, s[:n], b, scalars_mont=True, c=16, out=one, n=n)
+            torch.cuda.synchronize()
+            assert torch.equal(one[0], out[0]), group
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 @pytest.mark.parametrize("log_n", [21, 22])
 def test_msm_g1_chunk_scaling_sizes(amd, gh, log_n):
     """the accumulation chunk scales with the bucket size (16 at 2^21, 32 at 2^22, 128 at 2^24:
