@@ -81,65 +81,139 @@ struct RFq {
     }
 };
 
-// canonical r = t - p if t >= p else t   (t < 2p, canonical limbs)
+// Single-instruction lane ops whose carry / borrow lives in an SGPR lane mask.  A single wave
+// issuing a dependent chain pays ~6 cycles per instruction whatever the operation
+// (tools/latbench.hip), so the row arithmetic below is written for instruction COUNT: the carry
+// mask of v_add_co_u32 IS the generate ballot, and v_addc / v_subb / v_cndmask take the
+// lookahead result or a row-uniform flag directly as an SGPR mask (no per-lane bit extraction).
+namespace rowop {
+MBLS_DEV uint32_t add_co(uint32_t a, uint32_t b, uint64_t& carry) {
+    uint32_t r;
+    asm("v_add_co_u32_e64 %0, %1, %2, %3" : "=v"(r), "=s"(carry) : "v"(a), "v"(b));
+    return r;
+}
+MBLS_DEV uint32_t sub_co(uint32_t a, uint32_t b, uint64_t& borrow) {
+    uint32_t r;
+    asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r), "=s"(borrow) : "v"(a), "v"(b));
+    return r;
+}
+MBLS_DEV uint32_t add_mask(uint32_t a, uint64_t cin) {  // a + bit(cin, lane)
+    uint32_t r;
+    uint64_t c;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(c) : "v"(a), "s"(cin));
+    return r;
+}
+MBLS_DEV uint32_t sub_mask(uint32_t a, uint64_t bin) {  // a - bit(bin, lane)
+    uint32_t r;
+    uint64_t c;
+    asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(c) : "v"(a), "s"(bin));
+    return r;
+}
+MBLS_DEV uint32_t pick(uint64_t m, uint32_t if0, uint32_t if1) {  // bit(m, lane) ? if1 : if0
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(m));
+    return r;
+}
+// every lane of row r <- bit 16 r + 12 of B (the carry / borrow out of limb 11 of that row)
+MBLS_DEV uint64_t row_top_flag(uint64_t B) {
+    const uint64_t y = (B >> 12) & 0x0001000100010001ull;
+    return (y << 16) - y;  // row 3: the 2^64 term wraps away, leaving bits 48..63
+}
+}  // namespace rowop
+
+// canonical r = t - p if t >= p else t   (t < 2p, canonical 32-bit limbs, padding lanes 0)
 MBLS_DEV RFq rf_reduce_once(uint32_t t) {
-    const uint32_t p = RFq::mod_limb();
-    const uint64_t G = __ballot(t < p);   // borrow generated
-    const uint64_t E = __ballot(t == p);  // borrow propagated
+    // every row's top limb below p's: t < p, nothing to subtract (a wave-uniform branch; ~half
+    // of the sums of two canonical values)
+    if ((__ballot(t < RFq::mod_limb()) & 0x0800080008000800ull) == 0x0800080008000800ull) return {t};
+    uint64_t G;
+    const uint32_t d = rowop::sub_co(t, RFq::mod_limb(), G);  // G: borrow generated
+    const uint64_t E = __ballot(d == 0);                      // t_j == p_j: borrow propagated
     const uint64_t B = carries_in(G, E);
-    const uint32_t bin = (uint32_t)(B >> __lane_id()) & 1u;
-    const uint32_t d = t - p - bin;
-    // final borrow out of limb 11 == borrow into lane 12 of this row: t < p -> keep t
-    const bool lt = (B >> (rowdpp::row_shift() + 12)) & 1ull;
-    return {lt ? t : d};
+    const uint32_t r = rowop::sub_mask(d, B);
+    // borrow out of limb 11 (t < p): keep t.  Padding lanes: t = 0, and r = 0 when t >= p
+    return {rowop::pick(rowop::row_top_flag(B), r, t)};
 }
 
 // resolve a redundant per-lane value (lo + carry-from-below <= 2^33 - 2) to canonical limbs
 MBLS_DEV uint32_t rf_resolve(uint32_t lo, uint32_t carry_from_below) {
-    const uint64_t s = (uint64_t)lo + carry_from_below;
-    const uint32_t s_lo = (uint32_t)s;
-    const uint64_t G = __ballot((s >> 32) != 0);
-    const uint64_t P = __ballot(s_lo == 0xffffffffu);
-    const uint64_t C = carries_in(G, P);
-    return s_lo + ((uint32_t)(C >> __lane_id()) & 1u);
+    uint64_t G;
+    const uint32_t s = rowop::add_co(lo, carry_from_below, G);
+    const uint64_t P = __ballot(s == 0xffffffffu);
+    return rowop::add_mask(s, carries_in(G, P));
 }
 
 MBLS_DEV RFq operator+(const RFq& a, const RFq& b) {
-    const uint64_t s = (uint64_t)a.v + b.v;  // <= 2^33 - 2
-    const uint32_t t = rf_resolve((uint32_t)s, rowdpp::from_down((uint32_t)(s >> 32)));
-    return rf_reduce_once(t);
+    // a + b < 2p < 2^384: the limb carries ARE the generate mask, no shifted carry word
+    uint64_t G;
+    const uint32_t s = rowop::add_co(a.v, b.v, G);
+    const uint64_t P = __ballot(s == 0xffffffffu);
+    return rf_reduce_once(rowop::add_mask(s, carries_in(G, P)));
 }
 
 MBLS_DEV RFq operator-(const RFq& a, const RFq& b) {
-    const uint64_t G = __ballot(a.v < b.v);
-    const uint64_t E = __ballot(a.v == b.v);
+    uint64_t G;
+    const uint32_t d0 = rowop::sub_co(a.v, b.v, G);
+    const uint64_t E = __ballot(d0 == 0);
     const uint64_t B = carries_in(G, E);
-    const bool limb = rowdpp::lane16() < 12;
-    // padding lanes: the final borrow lands in lane 12 -- keep padding at zero
-    const uint32_t d = limb ? a.v - b.v - ((uint32_t)(B >> __lane_id()) & 1u) : 0u;
-    const bool neg = (B >> (rowdpp::row_shift() + 12)) & 1ull;
-    if (!neg) return {d};
-    // (a - b + 2^384) + p wraps past 2^384 exactly once: add lane-wise, drop the carry out
-    const uint64_t s = (uint64_t)d + RFq::mod_limb();
-    const uint32_t r = rf_resolve((uint32_t)s, rowdpp::from_down((uint32_t)(s >> 32)));
-    return {limb ? r : 0u};
+    const uint32_t d = rowop::sub_mask(d0, B);  // a - b mod 2^384 (padding lane 12: -1 if a < b)
+    const uint64_t neg = rowop::row_top_flag(B);
+    if (neg == 0) return {d};  // no row borrowed: skip the correction (a wave-uniform branch)
+    // a < b: (a - b + 2^384) + p wraps past 2^384 exactly once, which also clears lane 12
+    uint64_t G2;
+    const uint32_t e0 = rowop::add_co(d, RFq::mod_limb(), G2);
+    const uint64_t P2 = __ballot(e0 == 0xffffffffu);
+    const uint32_t e = rowop::add_mask(e0, carries_in(G2, P2));
+    return {rowop::pick(neg, d, e)};
 }
 
 MBLS_DEV RFq neg(const RFq& a) { return RFq::zero() - a; }
 MBLS_DEV RFq dbl(const RFq& a) { return a + a; }
 
-// lane-parallel CIOS Montgomery product
+// lane-parallel CIOS Montgomery product.  Round i, lane j:  v = a_j b_i + t_j,
+// m = lo(v_0) (-p^-1), w = m p_j + lo(v_j), t_j <- hi(v_j) + hi(w_j) + lo(w_{j+1}).
+// The round's dependent chain is what a lone wave pays for (tools/latbench.hip), so m is taken
+// from t_0 directly:  lo(v_0) (-p^-1) = lo(t_0) (-p^-1) + (a_0 (-p^-1)) b_i  (mod 2^32), one
+// v_mad_u64_u32 on the broadcast lo(t_0) with the addend a_0 (-p^-1) b_i computed off the chain,
+// while v = a b_i + t runs beside it:  bcast -> mad (m) -> mad (w) -> row shift -> add per round
+// instead of mad (v) -> bcast -> mul (m) -> mad (w) -> row shift -> add.
+MBLS_DEV uint32_t rf_mad_lo(uint32_t x, uint32_t y, uint32_t z) {  // lo(x*y + z) in ONE instruction
+    uint64_t r, c;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(c) : "v"(x), "s"(y), "v"((uint64_t)z));
+    return (uint32_t)r;
+}
+// 64-bit sum of two 32-bit values (opaque to the scheduler: keeps hi(v) + hi(w) off the row shift's
+// critical path instead of being reassociated behind it)
+MBLS_DEV uint64_t rf_add32x2(uint32_t x, uint32_t y) {
+    uint32_t lo, hi;
+    uint64_t c;
+    asm("v_add_co_u32_e64 %0, %2, %3, %4\n\tv_addc_co_u32_e64 %1, %2, 0, 0, %2"
+        : "=&v"(lo), "=v"(hi), "=&s"(c)
+        : "v"(x), "v"(y));
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+// (hi:lo) + x as a register pair, x 32-bit
+MBLS_DEV uint64_t rf_add64_32(uint64_t h, uint32_t x) {
+    uint32_t lo, hi;
+    uint64_t c;
+    asm("v_add_co_u32_e64 %0, %2, %3, %4\n\tv_addc_co_u32_e64 %1, %2, %5, 0, %2"
+        : "=&v"(lo), "=v"(hi), "=&s"(c)
+        : "v"((uint32_t)h), "v"(x), "v"((uint32_t)(h >> 32)));
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
 MBLS_DEV RFq operator*(const RFq& a, const RFq& b) {
     const uint32_t p = RFq::mod_limb();
+    const uint32_t ninv = __builtin_amdgcn_readfirstlane(FqCfg::NINV);
+    const uint32_t a0n = rowdpp::bcast<0>(a.v) * FqCfg::NINV;
     uint64_t t = 0;  // redundant: value = sum_j t_j 2^(32 j), t_j < 2^34
 #define MBLS_RF_ROW(I)                                                                    \
     {                                                                                     \
         const uint32_t bi = rowdpp::bcast<I>(b.v);                                        \
+        const uint32_t m = rf_mad_lo(rowdpp::bcast<0>((uint32_t)t), ninv, a0n * bi);      \
         const uint64_t v = (uint64_t)a.v * bi + t;                                        \
-        const uint32_t m = rowdpp::bcast<0>((uint32_t)v) * FqCfg::NINV;                   \
         const uint64_t w = (uint64_t)m * p + (uint32_t)v;                                 \
-        const uint64_t H = (uint64_t)(uint32_t)(v >> 32) + (uint32_t)(w >> 32);           \
-        t = H + rowdpp::from_up((uint32_t)w);                                             \
+        const uint64_t H = rf_add32x2((uint32_t)(v >> 32), (uint32_t)(w >> 32));          \
+        t = rf_add64_32(H, rowdpp::from_up((uint32_t)w));                                 \
     }
     MBLS_RF_ROW(0) MBLS_RF_ROW(1) MBLS_RF_ROW(2) MBLS_RF_ROW(3) MBLS_RF_ROW(4) MBLS_RF_ROW(5)
     MBLS_RF_ROW(6) MBLS_RF_ROW(7) MBLS_RF_ROW(8) MBLS_RF_ROW(9) MBLS_RF_ROW(10) MBLS_RF_ROW(11)

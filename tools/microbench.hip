@@ -70,6 +70,18 @@ __global__ void k_mont(uint32_t* out, const uint32_t* in, int iters) {
     store<C>(out + C::N * tid, s);
 }
 
+// inversion throughput: OP 0 binary GCD inv(), OP 1 Fermat
+template <class C, int OP>
+__global__ void k_inv(uint32_t* out, const uint32_t* in, int iters) {
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    Fp<C> x = load<C>(in + C::N * (tid & 1023));
+    for (int i = 0; i < iters; ++i) {
+        if constexpr (OP == 0) x = inv(x); else x = inv_fermat(x);
+        x.v[0] ^= 1;
+    }
+    store<C>(out + C::N * tid, x);
+}
+
 __global__ void k_copy(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -137,6 +149,36 @@ int main() {
             CK(hipMemcpy(hb, bad, 16, hipMemcpyDeviceToHost));
             printf("fips check mismatches: Fr mul %u sqr %u | Fq mul %u sqr %u (of %d each)\n", hb[0], hb[1], hb[2],
                    hb[3], 256 * 256 * 8);
+        }
+        // occupancy sweep (dynamic LDS caps the resident 256-thread blocks per CU at 1, 2, 3, 4):
+        // Fq fips::mul throughput with 1 and 2 independent chains per thread -> latency exposure
+        for (int occ = 1; occ <= 4; ++occ) {
+            size_t lds = (160 * 1024) / occ - 1024;
+            for (int ch = 1; ch <= 2; ++ch) {
+                auto kern = ch == 1 ? k_mont<FqCfg, 1, 1> : k_mont<FqCfg, 2, 1>;
+                hipLaunchKernelGGL(kern, blocks, threads, lds, 0, out, in, 4);
+                CK(hipDeviceSynchronize());
+                CK(hipEventRecord(e0));
+                hipLaunchKernelGGL(kern, blocks, threads, lds, 0, out, in, iters);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                double muls = (double)blocks * threads * iters * ch;
+                printf("occ %d waves/SIMD Fq fips mul x%d chains: %.3f ms, %.2f Gmul/s\n", occ, ch, ms, muls / ms / 1e6);
+            }
+        }
+        for (int op = 0; op < 2; ++op) {
+            auto kern = op == 0 ? k_inv<FqCfg, 0> : k_inv<FqCfg, 1>;
+            int it = 8;
+            hipLaunchKernelGGL(kern, blocks, threads, 0, 0, out, in, 1);
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL(kern, blocks, threads, 0, 0, out, in, it);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            double n = (double)blocks * threads * it;
+            printf("Fq inverse (%s): %.3f ms, %.3f Ginv/s\n", op == 0 ? "binary GCD" : "Fermat", ms, n / ms / 1e6);
         }
         RUN_MONT(FrCfg, 1, 0)
         RUN_MONT(FrCfg, 2, 0)
