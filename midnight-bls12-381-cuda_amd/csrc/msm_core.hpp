@@ -38,6 +38,7 @@
 #include "mbls_curve.hpp"
 #include "mbls_rowfield.hpp"
 #include "mbls_wavepoint.hpp"
+#include "mbls_lazy.hpp"
 #include "mbls_xyzz.hpp"
 
 #ifndef MBLS_XYZZ
@@ -151,6 +152,9 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
 //    over ONE round of resident waves: no partly filled last round, and ~1.3 partials per
 //    bucket at 2^20 instead of ~4 with 16-point chunks.
 // ------------------------------------------------------------------------------------
+#ifndef MBLS_LAZY_ACC
+#define MBLS_LAZY_ACC 0  // measured slower: 35 VGPR spills at the 3-wave bound
+#endif
 template <class F, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ chunk_off,
@@ -203,9 +207,18 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
     }
     (void)acc;
 #else
+    // G1: the accumulator lives in the lazy [0, 2p) representation (mbls_lazy.hpp) and is made
+    // canonical where it is stored
+    constexpr bool LAZY = std::is_same<L, Fq>::value && MBLS_LAZY_ACC;
+    auto flush = [&](const Jacobian<L>& a) {
+        if constexpr (LAZY)
+            store_jac<L>(partials, seg, lz::canon(a));
+        else
+            store_jac<L>(partials, seg, a);
+    };
     for (uint32_t e = beg; e < end; ++e) {
         if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
-            store_jac<L>(partials, seg, acc);
+            flush(acc);
             acc = Jacobian<L>::inf();
             do {
                 ++b;
@@ -215,11 +228,14 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
         }
         const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
         const Affine<L> pn = fetch(vn);
-        acc = jac_madd(acc, (v & 1) ? aff_neg(p) : p);
+        if constexpr (LAZY)
+            acc = lz::madd(acc, (v & 1) ? aff_neg(p) : p);
+        else
+            acc = jac_madd(acc, (v & 1) ? aff_neg(p) : p);
         v = vn;
         p = pn;
     }
-    store_jac<L>(partials, seg, acc);
+    flush(acc);
 #endif
 }
 
