@@ -522,7 +522,10 @@ eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hi
 //     Digit sources: NW words per index (GLV halves: 4 words, bit 127 = sign; plain: 8 words).
 // ------------------------------------------------------------------------------------
 static constexpr int DT_THREADS = 1024;
-static constexpr int DT_PER = 32;  // indices per thread
+#ifndef MBLS_DT_PER
+#define MBLS_DT_PER 16
+#endif
+static constexpr int DT_PER = MBLS_DT_PER;  // indices per thread
 static constexpr uint32_t DT_TILE = DT_THREADS * DT_PER;
 static constexpr uint32_t DT_MAX_B = 1u << 15;
 
@@ -873,7 +876,10 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __re
                                                             uint32_t* __restrict__ ent, uint32_t* __restrict__ seg_off,
                                                             uint32_t* __restrict__ seg_cnt,
                                                             uint32_t* __restrict__ part_tot, DigitOffset C) {
-    __shared__ uint32_t hist[256];
+    __shared__ uint32_t hist[256], tile_n;
+    // packed entries: the tile's slice of `ent` is assembled in LDS and written out in order
+    // (whole lines) instead of one random 4-byte store per contribution
+    __shared__ uint32_t stage[PACK ? DT_TILE : 1];
     constexpr int NW = SPLIT ? 4 : 8;
     const uint32_t tiles = (nidx + DT_TILE - 1) / DT_TILE;
     const uint32_t seg = blockIdx.x;  // w * tiles + tile
@@ -930,6 +936,7 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __re
             }
             run += h[k];
         }
+        if (l == 63) tile_n = run;  // entries of this tile
     }
     __syncthreads();
     const uint32_t fmask = (1u << FB) - 1;
@@ -940,11 +947,16 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __re
         if (idx >= nidx || v == 0) continue;
         const uint32_t part = (v - 1) >> FB, fine = (v - 1) & fmask;
         const uint32_t val = ((SPLIT ? idx : idx * F + f) << 1) | sign;
-        const size_t o = (size_t)seg * DT_TILE + hist[part] + lr[k];
         if (PACK)
-            ent[o] = FB ? (val | (fine << (32 - FB))) : val;
+            stage[hist[part] + lr[k]] = FB ? (val | (fine << (32 - FB))) : val;
         else
-            reinterpret_cast<uint2*>(ent)[o] = make_uint2(fine, val);
+            reinterpret_cast<uint2*>(ent)[(size_t)seg * DT_TILE + hist[part] + lr[k]] = make_uint2(fine, val);
+    }
+    if constexpr (PACK) {
+        __syncthreads();
+        const uint32_t nt = tile_n;
+        uint32_t* dst = ent + (size_t)seg * DT_TILE;
+        for (uint32_t i = threadIdx.x; i < nt; i += DT_THREADS) dst[i] = stage[i];
     }
 }
 
@@ -968,6 +980,12 @@ __device__ __forceinline__ void part_entry(const uint32_t* __restrict__ ent, siz
 #define MBLS_PS_TEAM 16
 #endif
 static constexpr uint32_t PS_TEAM = MBLS_PS_TEAM;
+// LDS stage of one part's span of `sorted`: 2^21 x 8 contributions over 8 x 256 parts average
+// 8192 entries per part at G1 2^20; 9216 words (36 KB) leave four workgroups per CU
+#ifndef MBLS_PS_STAGE
+#define MBLS_PS_STAGE 9216
+#endif
+static constexpr uint32_t PS_STAGE = MBLS_PS_STAGE;
 
 template <bool PACK>
 __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ ent, const uint32_t* __restrict__ seg_off,
@@ -976,7 +994,8 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
                                                    int Wg, uint32_t B, int FB, uint32_t NP,
                                                    uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets,
                                                    uint32_t* __restrict__ sorted) {
-    __shared__ uint32_t cnt[128], pre[128];
+    __shared__ uint32_t cnt[128], pre[128], span_sh;
+    __shared__ uint32_t ps_stage[PS_STAGE > 0 ? PS_STAGE : 1];
     const uint32_t FBN = 1u << FB;
     const uint32_t wl = blockIdx.x / NP, part = blockIdx.x % NP;
     // windows of group wl: wl, wl + Wg, ... < W (precompute factor F > 1), `tiles` segments each
@@ -1011,7 +1030,8 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
     if (threadIdx.x < 64) {  // wave 0: exclusive scan of the FBN <= 128 fine counts, 2 per lane
         const uint32_t l = threadIdx.x;
         const uint32_t h0 = 2 * l < FBN ? cnt[2 * l] : 0u, h1 = 2 * l + 1 < FBN ? cnt[2 * l + 1] : 0u;
-        const uint32_t run = wave_incl_scan(h0 + h1) - (h0 + h1);
+        const uint32_t incl = wave_incl_scan(h0 + h1), run = incl - (h0 + h1);
+        if (l == 63) span_sh = incl;  // this part's entry count
         const size_t key = (size_t)wl * B + part * FBN + 2 * l;
         if (2 * l < FBN) {
             pre[2 * l] = run;
@@ -1028,6 +1048,11 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
     __syncthreads();
     if (threadIdx.x < FBN) cnt[threadIdx.x] = 0;
     __syncthreads();
+    // the part's span of `sorted` is assembled in LDS and written out in order (whole lines),
+    // instead of one random 4-byte store per entry; a span larger than the stage (adversarial
+    // bucket skew) takes the direct stores
+    const uint32_t span = span_sh;
+    const bool staged = span <= PS_STAGE;
     for (uint32_t s = team; s < S; s += nteams) {
         const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
         const uint32_t k = seg_cnt[seg * NP + part];
@@ -1035,8 +1060,16 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
         for (uint32_t i = tl; i < k; i += PS_TEAM) {
             uint32_t fine, val;
             part_entry<PACK>(ent, o + i, FB, fine, val);
-            sorted[base + pre[fine] + atomicAdd(&cnt[fine], 1u)] = val;
+            const uint32_t pos = pre[fine] + atomicAdd(&cnt[fine], 1u);
+            if (staged)
+                ps_stage[pos] = val;
+            else
+                sorted[base + pos] = val;
         }
+    }
+    if (staged) {  // workgroup-uniform
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < span; i += blockDim.x) sorted[base + i] = ps_stage[i];
     }
 }
 
