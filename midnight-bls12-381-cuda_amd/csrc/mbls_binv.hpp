@@ -6,7 +6,13 @@
 // an MSM result).  The binary GCD needs no products in its inner loop: 31 steps run on 64-bit
 // approximations of (a, b) (exact low 31 bits, top 33 bits), recording the update matrix
 // (f0 g0; f1 g1); the 12-word values are then updated once per 31 steps with word-by-word
-// small-factor products.  ~25 outer steps for a 381-bit modulus.
+// small-factor products.  ~26 outer steps for a 381-bit modulus.
+//
+// GPU form (the one-lane normalisation is latency-bound): K = 30 inner steps per outer step so the
+// update factors satisfy |f|, |g| <= 2^30 and each pair (f, g) packs into ONE 64-bit word
+// f + g 2^32 (exact in two's complement, unpacked by sign extension) -- the pair updates are one
+// 64-bit subtract and one shift; the inner steps are unrolled and branch-free (the subtraction's
+// borrow is the a < b test); the bit length is taken once, of a | b, without a branch chain.
 //
 // Invariants (integers a, b >= 0; u, v mod m; y the input): a = u*y, b = v*y (mod m).  Start
 // a = y, b = m, u = 1, v = 0; each outer step maps (a, b) -> ((f0 a + g0 b) / 2^31, (f1 a + g1 b)
@@ -28,6 +34,8 @@
 namespace mbls {
 namespace binv {
 
+static constexpr int K = 30;  // inner steps per outer step
+
 template <int N>
 MBLS_HD bool is_zero(const uint32_t (&a)[N]) {
     uint32_t t = 0;
@@ -35,11 +43,16 @@ MBLS_HD bool is_zero(const uint32_t (&a)[N]) {
     return t == 0;
 }
 
+// bit length of a | b, i.e. max(bitlen(a), bitlen(b)), as a max over words (no branch chain)
 template <int N>
-MBLS_HD int bitlen(const uint32_t (&a)[N]) {
-    for (int i = N - 1; i >= 0; --i)
-        if (a[i]) return 32 * i + 32 - __builtin_clz(a[i]);
-    return 0;
+MBLS_HD int bitlen_or(const uint32_t (&a)[N], const uint32_t (&b)[N]) {
+    int n = 0;
+    for (int i = 0; i < N; ++i) {
+        const uint32_t w = a[i] | b[i];
+        const int l = w ? 32 * i + 32 - __builtin_clz(w | 1u) : 0;
+        n = l > n ? l : n;
+    }
+    return n;
 }
 
 // (a >> pos) & (2^33 - 1) for 0 <= pos, when a < 2^(pos + 33)
@@ -100,18 +113,18 @@ MBLS_HD bool signed_sum(uint32_t (&S)[M], const uint32_t (&P)[M], bool np, const
     return np;
 }
 
-// r = |f a + g b| / 2^31 (exact); returns true if f a + g b < 0.  |f|, |g| <= 2^31.
+// r = |f a + g b| / 2^K (exact); returns true if f a + g b < 0.  |f|, |g| <= 2^K.
 template <int N>
 MBLS_HD bool lincomb_shift(uint32_t (&r)[N], const uint32_t (&a)[N], const uint32_t (&b)[N], int64_t f, int64_t g) {
     uint32_t P[N + 1], Q[N + 1], S[N + 1];
     mul_small<N>(P, a, (uint32_t)(f < 0 ? -f : f));
     mul_small<N>(Q, b, (uint32_t)(g < 0 ? -g : g));
     const bool neg = signed_sum<N + 1>(S, P, f < 0, Q, g < 0);
-    for (int i = 0; i < N; ++i) r[i] = (S[i] >> 31) | (S[i + 1] << 1);
+    for (int i = 0; i < N; ++i) r[i] = (S[i] >> K) | (S[i + 1] << (32 - K));
     return neg && !is_zero<N>(r);
 }
 
-// r = (f u + g v) / 2^31 mod m, u, v in [0, m); result in [0, m).  |f|, |g| <= 2^31.
+// r = (f u + g v) / 2^K mod m, u, v in [0, m); result in [0, m).  |f|, |g| <= 2^K.
 template <int N>
 MBLS_HD void lincomb_mod(uint32_t (&r)[N], const uint32_t (&u)[N], const uint32_t (&v)[N], int64_t f, int64_t g,
                          const uint32_t (&m)[N], uint32_t ninv) {
@@ -119,27 +132,28 @@ MBLS_HD void lincomb_mod(uint32_t (&r)[N], const uint32_t (&u)[N], const uint32_
     mul_small<N>(P, u, (uint32_t)(f < 0 ? -f : f));
     mul_small<N>(Q, v, (uint32_t)(g < 0 ? -g : g));
     const bool neg = signed_sum<N + 1>(S, P, f < 0, Q, g < 0);
-    if (neg) {  // |S| < 2^32 m: S <- 2^32 m - |S|, in (0, 2^32 m]
+    if (neg) {  // |S| <= 2^(K+1) m: S <- 2^(K+1) m - |S|, in [0, 2^(K+1) m]
         int64_t br = 0;
         for (int i = 0; i <= N; ++i) {
-            const uint32_t mw = i == 0 ? 0u : m[i - 1];
+            const uint32_t lo = i == 0 ? 0u : m[i - 1] >> (31 - K);
+            const uint32_t mw = (i < N ? m[i] << (K + 1) : 0u) | lo;
             int64_t d = (int64_t)mw - S[i] + br;
             S[i] = (uint32_t)d;
             br = d >> 32;
         }
     }
-    // S + k m = 0 (mod 2^31), k = S * (-1/m) mod 2^31; S + k m < 3 * 2^31 m < 2^(32(N+1))
-    const uint32_t k = (S[0] * ninv) & 0x7fffffffu;
+    // S + k m = 0 (mod 2^K), k = S * (-1/m) mod 2^K; S + k m < 3 * 2^K m < 2^(32(N+1))
+    const uint32_t k = (S[0] * ninv) & ((1u << K) - 1);
     uint64_t c = 0;
     for (int i = 0; i <= N; ++i) {
         c += (uint64_t)S[i] + (i < N ? (uint64_t)m[i] * k : 0ull);
         S[i] = (uint32_t)c;
         c >>= 32;
     }
-    // (S + k m) / 2^31 < 3m: N + 1 words (3r > 2^256 for the 255-bit Fr modulus)
+    // (S + k m) / 2^K < 3m: N + 1 words (3r > 2^256 for the 255-bit Fr modulus)
     uint32_t t[N + 1];
-    for (int i = 0; i < N; ++i) t[i] = (S[i] >> 31) | (S[i + 1] << 1);
-    t[N] = S[N] >> 31;
+    for (int i = 0; i < N; ++i) t[i] = (S[i] >> K) | (S[i + 1] << (32 - K));
+    t[N] = S[N] >> K;
     for (int q = 0; q < 2; ++q) {
         uint32_t d[N + 1];
         int64_t br = 0;
@@ -155,7 +169,7 @@ MBLS_HD void lincomb_mod(uint32_t (&r)[N], const uint32_t (&u)[N], const uint32_
 }
 
 // out = 1 / y mod m (plain integers, y in [1, m), m odd, gcd(y, m) = 1).  Returns the number of
-// outer steps (<= 2 * bitlen(m) / 31 + 2 for valid input; capped so a bad input still ends).
+// outer steps (<= 2 * bitlen(m) / K + 2 for valid input; capped so a bad input still ends).
 template <int N>
 MBLS_HD int inverse(uint32_t (&out)[N], const uint32_t (&y)[N], const uint32_t (&m)[N], uint32_t ninv) {
     uint32_t a[N], b[N], u[N], v[N];
@@ -166,35 +180,29 @@ MBLS_HD int inverse(uint32_t (&out)[N], const uint32_t (&y)[N], const uint32_t (
         v[i] = 0;
     }
     int steps = 0;
-    const int cap = (64 * N) / 31 + 8;
+    const int cap = (64 * N) / K + 8;
     while (!is_zero<N>(a) && steps < cap) {
         ++steps;
-        const int la = bitlen<N>(a), lb = bitlen<N>(b);
-        const int n = la > lb ? (la > 64 ? la : 64) : (lb > 64 ? lb : 64);
+        const int nl = bitlen_or<N>(a, b);
+        const int n = nl > 64 ? nl : 64;
         uint64_t xa = (a[0] & 0x7fffffffu) | (top33<N>(a, n - 33) << 31);
         uint64_t xb = (b[0] & 0x7fffffffu) | (top33<N>(b, n - 33) << 31);
-        int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
-        for (int j = 0; j < 31; ++j) {
-            if (xa & 1) {
-                if (xa < xb) {
-                    const uint64_t t = xa;
-                    xa = xb;
-                    xb = t;
-                    int64_t s = f0;
-                    f0 = f1;
-                    f1 = s;
-                    s = g0;
-                    g0 = g1;
-                    g1 = s;
-                }
-                xa -= xb;
-                f0 -= f1;
-                g0 -= g1;
-            }
-            xa >>= 1;
-            f1 <<= 1;
-            g1 <<= 1;
+        // (f0, g0) and (f1, g1) packed as f + g 2^32 (two's complement, |f|, |g| <= 2^K)
+        uint64_t F0 = 1, F1 = 1ull << 32;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const bool odd = (xa & 1) != 0;
+            const bool lt = xa < xb;
+            const bool sw = odd && lt;
+            const uint64_t d = lt ? xb - xa : xa - xb;  // |xa - xb|: the new xa when odd
+            const uint64_t G0 = sw ? F1 : F0, G1 = sw ? F0 : F1;
+            xb = sw ? xa : xb;
+            xa = (odd ? d : xa) >> 1;
+            F0 = odd ? G0 - G1 : G0;
+            F1 = G1 << 1;
         }
+        int64_t f0 = (int32_t)(uint32_t)F0, g0 = ((int64_t)F0 - f0) >> 32;
+        int64_t f1 = (int32_t)(uint32_t)F1, g1 = ((int64_t)F1 - f1) >> 32;
         uint32_t na[N], nb[N], nu[N], nv[N];
         if (lincomb_shift<N>(na, a, b, f0, g0)) {
             f0 = -f0;

@@ -19,7 +19,7 @@ MBLS_DEV RFq rf_in(const uint32_t* in, int k) {
 }
 
 template <int OP>
-__global__ void k_rf(uint32_t* out, const uint32_t* in, int n) {
+__global__ __launch_bounds__(64) void k_rf(uint32_t* out, const uint32_t* in, int n) {
     RFq x = rf_in(in, 0), y = rf_in(in, 1);
     for (int i = 0; i < n; ++i) {
         if constexpr (OP == 0) x = x * y;
@@ -30,7 +30,7 @@ __global__ void k_rf(uint32_t* out, const uint32_t* in, int n) {
 }
 
 template <int OP>
-__global__ void k_wave(uint32_t* out, const uint32_t* in, int n) {
+__global__ __launch_bounds__(64) void k_wave(uint32_t* out, const uint32_t* in, int n) {
     Jacobian<RFq> p{rf_in(in, 0), rf_in(in, 1), rf_in(in, 2)}, q{rf_in(in, 3), rf_in(in, 4), rf_in(in, 5)};
     for (int i = 0; i < n; ++i) {
         if constexpr (OP == 0) p = wave::jdbl(p);
@@ -42,11 +42,24 @@ __global__ void k_wave(uint32_t* out, const uint32_t* in, int n) {
 }
 
 template <int OP>
-__global__ void k_lane(uint32_t* out, const uint32_t* in, int n) {
+__global__ __launch_bounds__(64) void k_lane(uint32_t* out, const uint32_t* in, int n) {
     Fq x = load<FqCfg>(in), y = load<FqCfg>(in + 12);
     for (int i = 0; i < n; ++i) {
         if constexpr (OP == 0) x = fips::mul(x, y);
         if constexpr (OP == 1) x = x + y;
+        if constexpr (OP == 2) x = inv(x) + y;  // binary GCD inversion chain
+        if constexpr (OP == 4) {                // the same on wave-uniform (SGPR, scalar-ALU) operands
+#pragma unroll
+            for (int k = 0; k < 12; ++k) x.v[k] = __builtin_amdgcn_readfirstlane(x.v[k]);
+            Fq z;
+            binv::inverse<12>(z.v, x.v, FqCfg::MOD, FqCfg::NINV);
+            x = z + y;
+        }
+        if constexpr (OP == 3) {                // the (x, y, 1) normalisation of one point
+            Jacobian<Fq> p{x, y, x + y};
+            Affine<Fq> a = jac_to_affine(p);
+            x = from_mont(a.x) + from_mont(a.y);
+        }
     }
     store<FqCfg>(out + 12 * threadIdx.x, x);
 }
@@ -69,6 +82,54 @@ __global__ void k_check(unsigned* bad, const uint32_t* in, int iters) {
         lb = l[2] - l[4];
         if (it % 7 == 3) { b = a; lb = la; }  // equal operands: a - b = 0, b - a = 0
     }
+}
+
+// pieces of one binary-GCD outer step, chained: OP 0 the 30 inner steps, 1 lincomb_shift,
+// 2 lincomb_mod, 3 bitlen + top33 approximations
+template <int OP>
+__global__ __launch_bounds__(64) void k_binv_part(uint32_t* out, const uint32_t* in, int n) {
+    uint32_t a[12], b[12];
+    for (int i = 0; i < 12; ++i) {
+        a[i] = in[i];
+        b[i] = in[12 + i];
+    }
+    uint64_t xa = ((uint64_t)a[1] << 32) | a[0], xb = ((uint64_t)b[1] << 32) | b[0];
+    int64_t f = 12345, g = -54321;
+    for (int it = 0; it < n; ++it) {
+        if constexpr (OP == 0) {
+            uint64_t F0 = 1, F1 = 1ull << 32;
+#pragma unroll
+            for (int j = 0; j < binv::K; ++j) {
+                const bool odd = (xa & 1) != 0;
+                const bool lt = xa < xb;
+                const bool sw = odd && lt;
+                const uint64_t d = lt ? xb - xa : xa - xb;
+                const uint64_t G0 = sw ? F1 : F0, G1 = sw ? F0 : F1;
+                xb = sw ? xa : xb;
+                xa = (odd ? d : xa) >> 1;
+                F0 = odd ? G0 - G1 : G0;
+                F1 = G1 << 1;
+            }
+            xa ^= F0 + F1 + 3;
+        } else if constexpr (OP == 1) {
+            uint32_t r[12];
+            if (binv::lincomb_shift<12>(r, a, b, f, g)) f = -f;
+            for (int i = 0; i < 12; ++i) a[i] = r[i] ^ in[i];
+        } else if constexpr (OP == 2) {
+            uint32_t r[12];
+            binv::lincomb_mod<12>(r, a, b, f, g, FqCfg::MOD, FqCfg::NINV);
+            for (int i = 0; i < 12; ++i) a[i] = r[i];
+        } else {
+            const int nl = binv::bitlen_or<12>(a, b);
+            const int nn = nl > 64 ? nl : 64;
+            xa += (a[0] & 0x7fffffffu) | (binv::top33<12>(a, nn - 33) << 31);
+            xb += (b[0] & 0x7fffffffu) | (binv::top33<12>(b, nn - 33) << 31);
+            a[(it & 3)] ^= (uint32_t)xa;
+        }
+    }
+    uint32_t o = (uint32_t)xa ^ (uint32_t)xb;
+    for (int i = 0; i < 12; ++i) o ^= a[i];
+    out[threadIdx.x] = o;
 }
 
 template <class K>
@@ -122,6 +183,13 @@ int main() {
     run("row Fq sub", k_rf<2>, out, in, 20000);
     run("lane Fq mul (fips)", k_lane<0>, out, in, 20000);
     run("lane Fq add", k_lane<1>, out, in, 20000);
+    run("lane Fq inverse (binary GCD)", k_lane<2>, out, in, 200);
+    run("lane jac_to_affine + from_mont", k_lane<3>, out, in, 200);
+    run("lane Fq inverse, uniform operands", k_lane<4>, out, in, 200);
+    run("binv: 30 inner steps", k_binv_part<0>, out, in, 2000);
+    run("binv: lincomb_shift", k_binv_part<1>, out, in, 2000);
+    run("binv: lincomb_mod", k_binv_part<2>, out, in, 2000);
+    run("binv: bitlen + top33 x2", k_binv_part<3>, out, in, 2000);
     run("wave jdbl", k_wave<0>, out, in, 2000);
     run("wave jadd", k_wave<1>, out, in, 2000);
     run("row jac_dbl", k_wave<2>, out, in, 2000);
