@@ -423,7 +423,10 @@ __global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict_
 
 // tree-sum stage: block b of window w sums V[w*m + k], k in [b*16*per_row, ...): each of the
 // 16 rows sums `per_row` consecutive points, then a 4-level LDS tree.  out[w*nblk + b].
-static constexpr int TREE_PER_ROW = 8;
+#ifndef MBLS_TREE_PER_ROW
+#define MBLS_TREE_PER_ROW 2  // 8 / 4 / 2: G2 2^20 12.81 / 12.66 / 12.64 ms, G1 reduction 1.02 / 1.01 / 1.00 ms
+#endif
+static constexpr int TREE_PER_ROW = MBLS_TREE_PER_ROW;
 template <class F>
 MBLS_DEV void tree_sum_block(const uint8_t* __restrict__ V, uint32_t m, uint32_t w, uint32_t blk, uint32_t per_row,
                              uint8_t* __restrict__ out, uint32_t out_idx) {
