@@ -76,6 +76,13 @@ eIcicleError plan_levels(MsmPlan& p, int Wl) {
         int v = e ? atoi(e) : SEG_LOG;
         return v >= 1 && v <= 6 ? v : SEG_LOG;
     }();
+    // G2: row segments of 8 and rows from 4096 segments (wave layout below): G2 2^20 12.69 ->
+    // 12.57 ms against 16 / 8192 (G1 keeps 16: 8 measured 1.026 vs 0.995 ms of reduction)
+    static const int row_log_g2 = [] {
+        const char* e = getenv("MBLS_ROW_SEG_LOG_G2");
+        int v = e ? atoi(e) : 3;
+        return v >= 1 && v <= 6 ? v : 3;
+    }();
     static const int wave_log = [] {
         const char* e = getenv("MBLS_WSEG_LOG");
         // measured (G1 2^20): 2 -> reduction 1.04 ms, 4 -> 1.12 ms once the narrow levels' tree
@@ -96,9 +103,10 @@ eIcicleError plan_levels(MsmPlan& p, int Wl) {
         int lg = SEG0_LOG, mode = MODE_LANE;
         const uint32_t lane_chains = ((m + (1u << SEG0_LOG) - 1) >> SEG0_LOG) * (uint32_t)Wl;
         if (p.levels > 0 || lane_chains < lane_min) {
-            const uint32_t row_chains = ((m + (1u << row_log) - 1) >> row_log) * (uint32_t)Wl;
+            const int rl = p.fq2 ? row_log_g2 : row_log;
+            const uint32_t row_chains = ((m + (1u << rl) - 1) >> rl) * (uint32_t)Wl;
             mode = row_chains >= wave_min_chains(p.fq2) ? MODE_ROW : MODE_WAVE;
-            lg = mode == MODE_ROW ? row_log : wave_log;
+            lg = mode == MODE_ROW ? rl : wave_log;
         }
         p.seg_log[p.levels] = (uint8_t)lg;
         p.mode[p.levels] = (uint8_t)mode;

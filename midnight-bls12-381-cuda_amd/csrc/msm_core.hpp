@@ -707,8 +707,8 @@ inline bool batch_pipeline() {  // read per call: the GPU tests switch it
 
 // reduction levels with fewer segments than this run one segment per wave (MBLS_WAVE_MIN tunes;
 // G2: MBLS_WAVE_MIN_G2).  An Fq2 row-sliced addition is three row products per Fq2 product in
-// series, so G2 switches to the wave layout (the three spread over rows) at more segments:
-// G2 2^20 level 1 (2048 segments of 16) 0.81 ms in rows.
+// series, so G2 switches to the wave layout (the three spread over rows) at more segments
+// (4096, with G2 row segments of 8: msm_common.hip plan_levels).
 inline uint32_t wave_min_chains(bool fq2 = false) {
     static const uint32_t v = [] {
         const char* e = getenv("MBLS_WAVE_MIN");
@@ -716,7 +716,7 @@ inline uint32_t wave_min_chains(bool fq2 = false) {
     }();
     static const uint32_t v2 = [] {
         const char* e = getenv("MBLS_WAVE_MIN_G2");
-        return e ? (uint32_t)atoi(e) : 8192u;
+        return e ? (uint32_t)atoi(e) : 4096u;
     }();
     return fq2 ? v2 : v;
 }
