@@ -31,6 +31,15 @@ struct Jacobian {
     }
 };
 
+// Where a square costs less than a product (the lane types: FIPS squaring computes each cross
+// product once) the formulas trade products for squares plus additions; the row-sliced types
+// square with a full product, so there the plain product saves the additions (mbls_rowfield.hpp
+// specialises this to false).  Same values either way.
+template <class F>
+struct SqrCheaper {
+    static constexpr bool value = true;
+};
+
 template <class F>
 MBLS_DEV Jacobian<F> jac_dbl(const Jacobian<F>& p) {
     // dbl-2009-l: 2M + 5S
@@ -38,8 +47,11 @@ MBLS_DEV Jacobian<F> jac_dbl(const Jacobian<F>& p) {
     F A = sqr(p.x);
     F B = sqr(p.y);
     F C = sqr(B);
-    F t = sqr(p.x + B) - A - C;
-    F D = dbl(t);
+    F D;
+    if constexpr (SqrCheaper<F>::value)
+        D = dbl(sqr(p.x + B) - A - C);  // 2((X + B)^2 - A - C) = 4 X B
+    else
+        D = dbl(dbl(p.x * B));
     F E = dbl(A) + A;
     F Fv = sqr(E);
     Jacobian<F> r;
@@ -76,7 +88,10 @@ MBLS_DEV Jacobian<F> jac_add(const Jacobian<F>& p, const Jacobian<F>& q) {
     Jacobian<F> r;
     r.x = sqr(R) - J - dbl(V);
     r.y = mul_sum(R, V - r.x, neg(dbl(S1)), J);
-    r.z = (sqr(p.z + q.z) - Z1Z1 - Z2Z2) * H;
+    if constexpr (SqrCheaper<F>::value)
+        r.z = (sqr(p.z + q.z) - Z1Z1 - Z2Z2) * H;  // 2 Z1 Z2 H
+    else
+        r.z = dbl((p.z * q.z) * H);
     return r;
 }
 

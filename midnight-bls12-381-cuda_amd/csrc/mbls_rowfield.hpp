@@ -15,6 +15,7 @@
 // Requirement: all 16 lanes of a row are active together (rows diverge only as a whole).
 #pragma once
 #include "mbls_field.hpp"
+#include "mbls_curve.hpp"
 
 namespace mbls {
 
@@ -270,6 +271,17 @@ MBLS_DEV RFq2 inv(const RFq2& a) {
     RFq n = inv(sqr(a.c0) + sqr(a.c1));
     return {a.c0 * n, neg(a.c1 * n)};
 }
+
+// a row-sliced square is a full row product: the curve formulas use products instead of
+// squares-plus-additions (mbls_curve.hpp SqrCheaper)
+template <>
+struct SqrCheaper<RFq> {
+    static constexpr bool value = false;
+};
+template <>
+struct SqrCheaper<RFq2> {
+    static constexpr bool value = false;
+};
 
 // ---- memory: element `idx` of an array of 48-byte Fq; each row loads one element ------
 MBLS_DEV RFq rf_load(const uint8_t* base, size_t idx) {

@@ -8,8 +8,8 @@
 // products of each dependency level of the formula are spread one per row (the row selects
 // its operands, computes one row product, and the 4 results are broadcast back to all rows by
 // ds_bpermute).  Additions/subtractions run replicated on every row.
-//   dbl-2009-l:  7 products in 3 levels      (row-serial: 7)
-//   add-2007-bl: 16 products in 5 levels     (row-serial: 16)
+//   dbl-2009-l:  7 products in 3 levels      (row-serial: 7; D = 4 X B as a product)
+//   add-2007-bl: 16 products in 5 levels     (row-serial: 16; Z3 = 2 (Z1 Z2) H)
 // Fq2 (G2) products expand into 3 Fq products (2 for squares) and a level's Fq products are
 // processed 4 at a time.  Results equal jac_dbl / jac_add exactly (same formulas, same
 // branches); only the schedule differs.
@@ -163,13 +163,14 @@ MBLS_DEV Jacobian<RF> jdbl(const Jacobian<RF>& p) {
     sqr_mul<2, 1>(s1, m1, {p.x, p.y}, {p.y}, {p.z});
     const RF A = s1[0], B = s1[1];
     const RF E = dbl(A) + A;
-    // L2: C = B^2, T = (X + B)^2, Fv = E^2
-    RF s2[3];
-    sqr<3>(s2, {B, p.x + B, E});
+    // L2: C = B^2, Fv = E^2 | XB = X*B  (D = 2((X + B)^2 - A - C) = 4 X B: a row product costs
+    // the same as a row square, and this form saves two additions)
+    RF s2[2], m2[1];
+    sqr_mul<2, 1>(s2, m2, {B, E}, {p.x}, {B});
     const RF C = s2[0];
-    const RF D = dbl(s2[1] - A - C);
+    const RF D = dbl(dbl(m2[0]));
     Jacobian<RF> r;
-    r.x = s2[2] - dbl(D);
+    r.x = s2[1] - dbl(D);
     // L3: E * (D - X3)
     RF m3[1];
     mul<1>(m3, {E}, {D - r.x});
@@ -183,9 +184,9 @@ template <class RF>
 MBLS_DEV Jacobian<RF> jadd(const Jacobian<RF>& p, const Jacobian<RF>& q) {
     if (p.is_inf()) return q;
     if (q.is_inf()) return p;
-    // L1: Z1Z1, Z2Z2, (Z1 + Z2)^2
-    RF s1[3];
-    sqr<3>(s1, {p.z, q.z, p.z + q.z});
+    // L1: Z1Z1, Z2Z2 | Z1Z2 (Z3 = 2 Z1 Z2 H instead of ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H)
+    RF s1[2], m1[1];
+    sqr_mul<2, 1>(s1, m1, {p.z, q.z}, {p.z}, {q.z});
     const RF Z1Z1 = s1[0], Z2Z2 = s1[1];
     // L2: U1 = X1 Z2Z2, U2 = X2 Z1Z1, Z2^3, Z1^3
     RF m2[4];
@@ -203,13 +204,13 @@ MBLS_DEV Jacobian<RF> jadd(const Jacobian<RF>& p, const Jacobian<RF>& q) {
     }
     const RF I = s3[0];
     R = dbl(R);
-    // L4: RR = R^2 | J = H I, V = U1 I, Z3 = ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H
+    // L4: RR = R^2 | J = H I, V = U1 I, Z1Z2 H (Z3 = 2 Z1Z2 H)
     RF s4[1], m4[3];
-    sqr_mul<1, 3>(s4, m4, {R}, {H, U1, s1[2] - Z1Z1 - Z2Z2}, {I, I, H});
+    sqr_mul<1, 3>(s4, m4, {R}, {H, U1, m1[0]}, {I, I, H});
     const RF J = m4[0], V = m4[1];
     Jacobian<RF> r;
     r.x = s4[0] - J - dbl(V);
-    r.z = m4[2];
+    r.z = dbl(m4[2]);
     // L5: R (V - X3), S1 J
     RF m5[2];
     mul<2>(m5, {R, S1}, {V - r.x, J});

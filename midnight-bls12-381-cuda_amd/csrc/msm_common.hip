@@ -83,6 +83,11 @@ eIcicleError plan_levels(MsmPlan& p, int Wl) {
         int v = e ? atoi(e) : 3;
         return v >= 1 && v <= 6 ? v : 3;
     }();
+    static const int seg0_log = [] {  // level 0, one segment per lane (MBLS_SEG0_LOG)
+        const char* e = getenv("MBLS_SEG0_LOG");
+        int v = e ? atoi(e) : SEG0_LOG;
+        return v >= 1 && v <= 6 ? v : SEG0_LOG;
+    }();
     static const int wave_log = [] {
         const char* e = getenv("MBLS_WSEG_LOG");
         // measured (G1 2^20): 2 -> reduction 1.04 ms, 4 -> 1.12 ms once the narrow levels' tree
@@ -100,8 +105,8 @@ eIcicleError plan_levels(MsmPlan& p, int Wl) {
     uint32_t m = p.B;
     while (true) {
         if (p.levels >= MAX_LEVELS) return MBLS_INVALID_ARGUMENT;
-        int lg = SEG0_LOG, mode = MODE_LANE;
-        const uint32_t lane_chains = ((m + (1u << SEG0_LOG) - 1) >> SEG0_LOG) * (uint32_t)Wl;
+        int lg = seg0_log, mode = MODE_LANE;
+        const uint32_t lane_chains = ((m + (1u << seg0_log) - 1) >> seg0_log) * (uint32_t)Wl;
         if (p.levels > 0 || lane_chains < lane_min) {
             const int rl = p.fq2 ? row_log_g2 : row_log;
             const uint32_t row_chains = ((m + (1u << rl) - 1) >> rl) * (uint32_t)Wl;
