@@ -121,6 +121,26 @@ MBLS_DEV Jacobian<F> jac_madd(const Jacobian<F>& p, const Affine<F>& q) {
     return r;
 }
 
+// affine + affine (p.z == 1): mmadd-2007-bl, 4M + 2S with Y3 as one lazy product sum -- the
+// formula madd-2007-bl reduces to at Z1 = 1 (Z1Z1 = 1, U2 = X2, S2 = Y2, Z3 = (1 + H)^2 - 1 - HH
+// = 2H), so the result is the same projective representative jac_madd returns.  The second
+// point of every accumulation chunk meets an accumulator fresh from its first point.  Returns
+// false (r untouched) when x1 == x2 (equal or opposite points), left to jac_madd's branches.
+template <class F>
+MBLS_DEV bool jac_mmadd(const Jacobian<F>& p, const Affine<F>& q, Jacobian<F>& r) {
+    const F H = q.x - p.x;
+    if (H.is_zero()) return false;
+    const F HH = sqr(H);
+    const F I = dbl(dbl(HH));
+    const F J = H * I;
+    const F R = dbl(q.y - p.y);
+    const F V = p.x * I;
+    r.x = sqr(R) - J - dbl(V);
+    r.y = mul_sum(R, V - r.x, neg(dbl(p.y)), J);
+    r.z = dbl(H);
+    return true;
+}
+
 template <class F>
 MBLS_DEV Affine<F> aff_neg(const Affine<F>& a) {
     if (a.is_inf()) return a;

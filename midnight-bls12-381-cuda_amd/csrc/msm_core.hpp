@@ -152,6 +152,9 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
 //    over ONE round of resident waves: no partly filled last round, and ~1.3 partials per
 //    bucket at 2^20 instead of ~4 with 16-point chunks.
 // ------------------------------------------------------------------------------------
+#ifndef MBLS_ACC_MMADD
+#define MBLS_ACC_MMADD 1
+#endif
 #ifndef MBLS_LAZY_ACC
 #define MBLS_LAZY_ACC 0  // measured slower: 35 VGPR spills at the 3-wave bound
 #endif
@@ -228,10 +231,18 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
         }
         const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
         const Affine<L> pn = fetch(vn);
-        if constexpr (LAZY)
-            acc = lz::madd(acc, (v & 1) ? aff_neg(p) : p);
-        else
-            acc = jac_madd(acc, (v & 1) ? aff_neg(p) : p);
+        const Affine<L> q = (v & 1) ? aff_neg(p) : p;
+        // second point of the chunk (the same step for every lane of the wave): the accumulator
+        // is still the first point, Z = 1, so the affine + affine formula applies (~55% of a
+        // mixed addition); a bucket boundary at this step left it at the identity instead
+        bool done = false;
+        if (MBLS_ACC_MMADD && !LAZY && e == beg + 1 && !acc.is_inf() && !q.is_inf()) done = jac_mmadd(acc, q, acc);
+        if (!done) {
+            if constexpr (LAZY)
+                acc = lz::madd(acc, q);
+            else
+                acc = jac_madd(acc, q);
+        }
         v = vn;
         p = pn;
     }
