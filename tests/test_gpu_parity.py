@@ -359,6 +359,43 @@ def test_msm_adversarial_heavy_buckets(amd, gh, c):
     assert gh.decode_icicle("g1", out[0]) == H.g1_from_affine_mont(ref)
 
 
+@pytest.mark.parametrize("group", ["g1", "g2"])
+def test_msm_chunk_start_exceptional_pairs(amd, gh, group):
+    """the accumulation adds a chunk's second point with the affine + affine formula (its first
+    point left the accumulator at Z = 1): equal points (doubling), opposite points (identity) and
+    identity bases must reach that step.  All bases equal (every chunk opens with P + P), +-P
+    alternating with equal scalars (P + (-P)), and a pattern with identities, vs the oracle."""
+    import torch
+    n = 4096
+    nl = 12 if group == "g1" else 24
+    one = torch.zeros((1, nl), dtype=torch.int64, device="cuda")
+    amd.gen_bases(group, one, 4242)
+    pt = amd.to_numpy_u64(one)[0]
+    half = nl // 2
+    y = pr.limbs_to_int([int(v) for v in pt[half:half + 6]])
+    neg = pt.copy()
+    neg[half:half + 6] = pr.int_to_limbs((pr.P - y) % pr.P, 6)
+    if group == "g2":  # y = (y0, y1): negate both components
+        y1 = pr.limbs_to_int([int(v) for v in pt[half + 6:]])
+        neg[half + 6:] = pr.int_to_limbs((pr.P - y1) % pr.P, 6)
+    zero = np.zeros(nl, dtype=np.uint64)
+    rnd = np.random.default_rng(11)
+    s_rand = H.ints_to_limbs([int(rnd.integers(1, 2 ** 62)) * int(rnd.integers(1, 2 ** 62)) * int(rnd.integers(1, 2 ** 62)) % pr.R
+                              for _ in range(n)], 4)
+    s_same = H.ints_to_limbs([pr.R - 77777] * n, 4)
+    cases = [
+        ("all equal", np.tile(pt, (n, 1)), s_rand),
+        ("+-P alternating, equal scalars", np.stack([pt if i % 2 == 0 else neg for i in range(n)]), s_same),
+        ("P, P, identity, -P pattern", np.stack([(pt, pt, zero, neg)[i % 4] for i in range(n)]), s_rand),
+    ]
+    for name, bases, scal in cases:
+        bases = np.ascontiguousarray(bases.astype(np.uint64))
+        out = amd.msm(group, amd.torch_u64(scal), amd.torch_u64(bases), icicle=True, n=n)
+        ref = H.oracle_msm(group, scal, bases)
+        want = H.g1_from_affine_mont(ref) if group == "g1" else H.g2_from_affine_mont(ref)
+        assert gh.decode_icicle(group, out[0]) == want, name
+
+
 def test_msm_precompute_factor(amd, gh):
     g = H.load_golden("msm_g1.json")
     case = [c for c in g["cases"] if c["name"] == "random_300"][0]
