@@ -1142,12 +1142,17 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         lvoff += (size_t)m_out * P.Wg;
     }
     if (njobs) hipLaunchKernelGGL(k_tree_sum_jobs<F>, dim3(njobs * P.Wg), dim3(256), 0, st, jobs, P.Wg);
-    // join the side streams (the first also carried the table / heavy-bucket work)
-    for (int k = 0; k < TREE_SIDES && use_side; ++k) {
-        if (!used[k] && k > 0) continue;
-        hipEvent_t je = k == 0 ? ctx.events[P.levels] : ev[3 + k];
-        MBLS_TRY(hipEventRecord(je, ctx.sides[k]));
-        MBLS_TRY(hipStreamWaitEvent(st, je, 0));
+    // join the side streams (the first also carried the table / heavy-bucket work): the others
+    // fold into side 0, so the main stream waits once (each wait on it is a barrier packet,
+    // ~5 us of gap ahead of the window Horner)
+    if (use_side) {
+        for (int k = 1; k < TREE_SIDES; ++k) {
+            if (!used[k]) continue;
+            MBLS_TRY(hipEventRecord(ev[3 + k], ctx.sides[k]));
+            MBLS_TRY(hipStreamWaitEvent(ctx.sides[0], ev[3 + k], 0));
+        }
+        MBLS_TRY(hipEventRecord(ctx.events[P.levels], ctx.sides[0]));
+        MBLS_TRY(hipStreamWaitEvent(st, ctx.events[P.levels], 0));
     }
     hipLaunchKernelGGL((k_window_horner<F, MODE_WAVE>), dim3(P.Wg), dim3(64), 0, st, sums, P.levels, P.Wg,
                        P.seg_logs_packed(), windows);
