@@ -148,9 +148,10 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
 // ------------------------------------------------------------------------------------
 // 4. accumulation: thread t sums the L contributions at sorted positions [L t, L t + L),
 //    one partial per bucket segment it touches (see k_chunk_counts): no idle lanes on the
-//    short last chunk of each bucket.  L (accumulate_chunk) spreads the contributions evenly
-//    over ONE round of resident waves: no partly filled last round, and ~1.3 partials per
-//    bucket at 2^20 instead of ~4 with 16-point chunks.
+//    short last chunk of each bucket.  L = accumulate_chunk: max(16, contributions per bucket
+//    / 8) -- 16 at 2^20 (one 64-byte line of sorted indices per thread, ~5 partials per
+//    bucket), growing with the buckets at 2^22+ so they stay off the heavy-bucket passes
+//    (MBLS_ACC_CHUNK=auto: one round of resident waves, measured slower at 2^20).
 // ------------------------------------------------------------------------------------
 #ifndef MBLS_ACC_MMADD
 #define MBLS_ACC_MMADD 1
