@@ -77,7 +77,7 @@ eIcicleError plan_levels(MsmPlan& p, int Wl) {
         return v >= 1 && v <= 6 ? v : SEG_LOG;
     }();
     // G2: row segments of 8 and rows from 4096 segments (wave layout below): G2 2^20 12.69 ->
-    // 12.57 ms against 16 / 8192 (G1 keeps 16: 8 measured 1.026 vs 0.995 ms of reduction)
+    // 12.57 ms against 16 / 8192 (G1: segments of 8 too since the 2-point tree rows, SEG_LOG)
     static const int row_log_g2 = [] {
         const char* e = getenv("MBLS_ROW_SEG_LOG_G2");
         int v = e ? atoi(e) : 3;
