@@ -502,16 +502,21 @@ __global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, in
 
 // final fold over window groups: sum_w 2^(c w) G_w  (one chain)
 template <class F, int MODE>
-__global__ void k_final(const uint8_t* __restrict__ windows, int Wg, int c, uint8_t* __restrict__ result) {
-    MBLS_TAIL_PRIO();
+MBLS_DEV auto final_fold(const uint8_t* __restrict__ windows, int Wg, int c) {
     using IO = RedIO<F, MODE>;
-    if (IO::id() != 0) return;
     auto acc = IO::ld(windows, Wg - 1);
     for (int w = Wg - 2; w >= 0; --w) {
         for (int k = 0; k < c; ++k) acc = IO::dbl(acc);
         acc = IO::add(acc, IO::ld(windows, w));
     }
-    IO::st(result, 0, acc);
+    return acc;
+}
+template <class F, int MODE>
+__global__ void k_final(const uint8_t* __restrict__ windows, int Wg, int c, uint8_t* __restrict__ result) {
+    MBLS_TAIL_PRIO();
+    using IO = RedIO<F, MODE>;
+    if (IO::id() != 0) return;
+    IO::st(result, 0, final_fold<F, MODE>(windows, Wg, c));
 }
 
 // window-group fold chain (msm_device, groups > 1): acc = 2^ndbl acc, then acc += H_g (acc = H_g
@@ -591,10 +596,7 @@ MBLS_DEV RFq2 one_std<RFq2>() {
 // (launched with 64 threads: the bound lets the inversion keep its words in VGPRs -- at the
 // default 1024-thread bound it spilled 204 B (G1) / 912 B (G2) to scratch)
 template <class F>
-__global__ __launch_bounds__(64) void k_jac_to_icicle(uint8_t* pts, int count) {
-    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (i >= count) return;
-    Jacobian<F> p = load_jac<F>(pts, i);
+MBLS_DEV void icicle_point(const Jacobian<F>& p, uint8_t* out, size_t i) {
     Jacobian<F> o;
     if (p.is_inf()) {
         o.x = F::zero();
@@ -606,7 +608,39 @@ __global__ __launch_bounds__(64) void k_jac_to_icicle(uint8_t* pts, int count) {
         o.y = from_mont_f(a.y);
         o.z = one_std<F>();
     }
-    store_jac<F>(pts, i, o);
+    store_jac<F>(out, i, o);
+}
+
+// in and out may alias (in place)
+template <class F>
+__global__ __launch_bounds__(64) void k_jac_to_icicle(const uint8_t* in, uint8_t* out, int count) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= count) return;
+    icicle_point<F>(load_jac<F>(in, i), out, i);
+}
+
+// a row-sliced value (limb j on lane j of every row) gathered into one lane's limbs
+MBLS_DEV Fq row_to_lane(const RFq& a) {
+    Fq r;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r.v[i] = (uint32_t)__shfl((int)a.v, i, 64);
+    return r;
+}
+MBLS_DEV Fq2 row_to_lane(const RFq2& a) { return {row_to_lane(a.c0), row_to_lane(a.c1)}; }
+
+// k_final + k_jac_to_icicle in one launch (single ICICLE MSM, result on device): the wave's
+// folded point is gathered into lane 0, which normalises it and writes ICICLE's (x, y, 1)
+// straight into the caller's buffer (one launch gap and the result copy fewer)
+template <class F>
+__global__ __launch_bounds__(64) void k_final_icicle(const uint8_t* __restrict__ windows, int Wg, int c,
+                                                     uint8_t* __restrict__ out) {
+    MBLS_TAIL_PRIO();
+    const RJac<F> acc = final_fold<F, MODE_WAVE>(windows, Wg, c);
+    Jacobian<F> p;
+    p.x = row_to_lane(acc.x);
+    p.y = row_to_lane(acc.y);
+    p.z = row_to_lane(acc.z);
+    if (threadIdx.x == 0) icicle_point<F>(p, out, 0);
 }
 
 template <class F>
@@ -913,12 +947,13 @@ inline int msm_groups() {  // read per call: the GPU tests switch it
 template <class F>
 eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t* bases, uint32_t n,
                         const MsmPlan& P, uint8_t* result, StreamCtx& ctx, hipStream_t st, bool use_side = true,
-                        hipEvent_t acc_done = nullptr) {
+                        hipEvent_t acc_done = nullptr, uint8_t* icicle_out = nullptr) {
     Arena& arena = ctx.arena;
     constexpr size_t JAC = GroupTraits<F>::JAC, AFF = GroupTraits<F>::AFF;
     constexpr uint32_t LN = LaneOf<F>::LANES;  // lanes per chain in the lane-mode kernels
     if (n == 0) {
         hipLaunchKernelGGL(k_store_inf<F>, dim3(1), dim3(64), 0, st, result, 1);
+        if (icicle_out) hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3(1), dim3(64), 0, st, result, icicle_out, 1);
         MBLS_TRY(hipGetLastError());
         return MBLS_SUCCESS;
     }
@@ -1063,6 +1098,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             ProfScope ps("msm.tail", st);  // exposed tail: last accumulation -> fold done
             MBLS_TRY(hipStreamWaitEvent(st, gev[2 * G], 0));
         }
+        if (icicle_out) hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3(1), dim3(64), 0, st, result, icicle_out, 1);
         MBLS_TRY(hipGetLastError());
         return MBLS_SUCCESS;
     }
@@ -1159,7 +1195,10 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
                        P.seg_logs_packed(), windows);
     {
         ProfScope ps("msm.final", st);
-        hipLaunchKernelGGL((k_final<F, MODE_WAVE>), dim3(1), dim3(64), 0, st, windows, P.Wg, P.c, result);
+        if (icicle_out)
+            hipLaunchKernelGGL(k_final_icicle<F>, dim3(1), dim3(64), 0, st, windows, P.Wg, P.c, icicle_out);
+        else
+            hipLaunchKernelGGL((k_final<F, MODE_WAVE>), dim3(1), dim3(64), 0, st, windows, P.Wg, P.c, result);
     }
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
@@ -1264,17 +1303,28 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
             MBLS_TRY(hipStreamWaitEvent(st, ctx.pipe_ev[1 + k], 0));
         }
     } else {
+        // one ICICLE MSM with its result on the device: the final fold writes the normalised
+        // (x, y, 1) straight into `results` (k_final_icicle; 16-byte stores, so aligned buffers only)
+        uint8_t* direct = (entry == MSM_ICICLE && batch == 1 && cfg->are_results_on_device &&
+                           ((uintptr_t)results & 15) == 0)
+                              ? (uint8_t*)results
+                              : nullptr;
         const size_t mark = A.mark();
         for (int b = 0; b < batch; ++b) {
             A.rewind(mark);  // scratch reused across the batch (stream-ordered)
             const uint8_t* sb = d_s + (size_t)b * n * 32;
             const uint8_t* bb = d_b + (shared ? 0 : (size_t)b * nbases_per * AFF);
-            er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, ctx, st);
+            er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, ctx, st, true, nullptr, direct);
             if (er != MBLS_SUCCESS) return er;
+        }
+        if (direct) {
+            MBLS_TRY(hipGetLastError());
+            if (!cfg->is_async || st_s || (st_b && !cfg->are_points_on_device)) MBLS_TRY(hipStreamSynchronize(st));
+            return MBLS_SUCCESS;
         }
     }
     if (entry == MSM_ICICLE) {
-        hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch + 63) / 64), dim3(64), 0, st, d_r, batch);
+        hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch + 63) / 64), dim3(64), 0, st, d_r, d_r, batch);
         MBLS_TRY(hipGetLastError());
     }
     MBLS_TRY(hipMemcpyAsync(results, d_r, JAC * (size_t)batch,

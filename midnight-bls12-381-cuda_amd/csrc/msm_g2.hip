@@ -46,7 +46,7 @@ eIcicleError mbls_g2_sum_jacobian(const mbls_g2_projective_t* pts, int count, mb
 eIcicleError mbls_g2_jacobian_to_icicle(mbls_g2_projective_t* pts, int count, void* stream) {
     if (!pts || count < 0) return MBLS_INVALID_ARGUMENT;
     if (count == 0) return MBLS_SUCCESS;
-    hipLaunchKernelGGL(k_jac_to_icicle<G>, dim3((count + 63) / 64), dim3(64), 0, (hipStream_t)stream, (uint8_t*)pts,
+    hipLaunchKernelGGL(k_jac_to_icicle<G>, dim3((count + 63) / 64), dim3(64), 0, (hipStream_t)stream, (const uint8_t*)pts, (uint8_t*)pts,
                        count);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
