@@ -101,13 +101,19 @@ eIcicleError plan_levels(MsmPlan& p, int Wl) {
         const char* e = getenv("MBLS_LANE_MIN");
         return e ? (uint32_t)atoi(e) : 32768u;
     }();
+    // levels [0, lane_levels) may run one segment per lane (MBLS_LANE_LEVELS, default 1)
+    static const int lane_levels = [] {
+        const char* e = getenv("MBLS_LANE_LEVELS");
+        int v = e ? atoi(e) : 1;
+        return v >= 1 && v <= 4 ? v : 1;
+    }();
     p.levels = 0;
     uint32_t m = p.B;
     while (true) {
         if (p.levels >= MAX_LEVELS) return MBLS_INVALID_ARGUMENT;
         int lg = seg0_log, mode = MODE_LANE;
         const uint32_t lane_chains = ((m + (1u << seg0_log) - 1) >> seg0_log) * (uint32_t)Wl;
-        if (p.levels > 0 || lane_chains < lane_min) {
+        if (p.levels >= lane_levels || lane_chains < lane_min) {
             const int rl = p.fq2 ? row_log_g2 : row_log;
             const uint32_t row_chains = ((m + (1u << rl) - 1) >> rl) * (uint32_t)Wl;
             mode = row_chains >= wave_min_chains(p.fq2) ? MODE_ROW : MODE_WAVE;
