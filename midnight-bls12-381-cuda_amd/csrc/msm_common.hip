@@ -1153,10 +1153,16 @@ MBLS_DEV uint32_t order_index(uint32_t blk, uint32_t bin, uint32_t bpg) {
     return (blk / bpg) * (ORDER_BINS * bpg) + (SMALL_MAX - bin) * bpg + blk % bpg;
 }
 
-__global__ void k_chunk_counts(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offsets,
-                               uint32_t* __restrict__ nchunks, uint32_t m, uint32_t L, uint32_t* __restrict__ binhist,
-                               uint32_t bpg) {
+// also the first half of the chunk_off scan: cloc[b] = exclusive prefix of the chunk counts
+// inside b's block of 256 buckets, blk_tot[block] = the block's total (k_scan_small scans the
+// totals, k_chunk_owner adds the prefixes: no separate 3-kernel scan).  cloc may alias counts
+// (each thread reads its count before writing its prefix).
+__global__ __launch_bounds__(256) void k_chunk_counts(const uint32_t* counts, const uint32_t* __restrict__ offsets,
+                                                      uint32_t* __restrict__ nchunks, uint32_t m, uint32_t L,
+                                                      uint32_t* __restrict__ binhist, uint32_t bpg, uint32_t* cloc,
+                                                      uint32_t* __restrict__ blk_tot) {
     __shared__ uint32_t hist[ORDER_BINS];
+    __shared__ uint32_t wsum[4];
     if (threadIdx.x < ORDER_BINS) hist[threadIdx.x] = 0;
     __syncthreads();
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1166,6 +1172,20 @@ __global__ void k_chunk_counts(const uint32_t* __restrict__ counts, const uint32
         c = cnt ? (o + cnt - 1) / L - o / L + 1 : 0u;
         nchunks[b] = c;
         if (c <= SMALL_MAX) atomicAdd(&hist[c], 1u);
+    }
+    {
+        const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        uint32_t incl = c;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(incl, d, 64);
+            if (lane >= (uint32_t)d) incl += t;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t base = 0;
+        for (uint32_t k = 0; k < w; ++k) base += wsum[k];
+        if (b < m) cloc[b] = base + incl - c;
+        if (threadIdx.x == 0) blk_tot[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     }
     // block max, then at most one atomic per block and only when it raises the running max
     // (4096 same-address atomics cost 46 us at 2^20; the filtered read is monotone-safe)
@@ -1187,24 +1207,22 @@ __global__ void k_chunk_counts(const uint32_t* __restrict__ counts, const uint32
 // scan of k_chunk_counts' histograms (order_index layout).
 
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
-                                 uint32_t L, uint32_t* binhist, uint32_t groups, bool zeroed, hipStream_t st) {
+                                 uint32_t L, uint32_t* binhist, uint32_t groups, bool zeroed, uint32_t* cloc,
+                                 uint32_t* blk_tot, hipStream_t st) {
     if (!zeroed) MBLS_TRY(hipMemsetAsync(nchunks + m, 0, 4, st));
     const uint32_t nblk = (m + 255) / 256;
     hipLaunchKernelGGL(k_chunk_counts, dim3(nblk), dim3(256), 0, st, counts, offsets, nchunks, m, L, binhist,
-                       nblk / groups);
+                       nblk / groups, cloc, blk_tot);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }
 
 uint32_t order_words(uint32_t m) { return ORDER_BINS * ((m + 255) / 256); }
 
-// exclusive scan of a short array (the order histograms, ~17 K words) in ONE workgroup; out[m]
-// = total
-__global__ __launch_bounds__(1024) void k_scan_small(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                     uint32_t m) {
-    __shared__ uint32_t wtot[16];
+// exclusive scan of a short array in ONE workgroup of 1024 threads; out[m] = total
+MBLS_DEV void scan_wg(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t m, uint32_t* wtot) {
     const uint32_t per = (m + 1023) / 1024;
-    const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, m);
+    const uint32_t b0 = min(threadIdx.x * per, m), b1 = min(b0 + per, m);
     uint32_t a = 0;
     for (uint32_t k = b0; k < b1; ++k) a += in[k];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1224,10 +1242,23 @@ __global__ __launch_bounds__(1024) void k_scan_small(const uint32_t* __restrict_
         run += v;
     }
     if (threadIdx.x == 1023) out[m] = run;
+    __syncthreads();  // wtot is reused by the next scan
 }
 
-eIcicleError launch_order_scan(const uint32_t* binhist, uint32_t* binbase, uint32_t m, hipStream_t st) {
-    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, binhist, binbase, order_words(m));
+// the order histograms (~17 K words) and the chunk-count block totals (k_chunk_counts), one
+// workgroup for both
+__global__ __launch_bounds__(1024) void k_scan_small(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                     uint32_t m, const uint32_t* __restrict__ in2,
+                                                     uint32_t* __restrict__ out2, uint32_t m2) {
+    __shared__ uint32_t wtot[16];
+    scan_wg(in, out, m, wtot);
+    scan_wg(in2, out2, m2, wtot);
+}
+
+eIcicleError launch_order_scan(const uint32_t* binhist, uint32_t* binbase, uint32_t m, const uint32_t* blk_tot,
+                               uint32_t* blk_pre, hipStream_t st) {
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, binhist, binbase, order_words(m), blk_tot, blk_pre,
+                       (m + 255) / 256);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }
@@ -1253,18 +1284,24 @@ eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const ui
     return MBLS_SUCCESS;
 }
 
-// owner[segment] = bucket; first[t] = the bucket holding position L t (the start of chunk t);
-// and the bucket order of k_bucket_order (same grid: one thread per bucket)
-__global__ void k_chunk_owner(const uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ offsets, uint32_t m,
-                              uint32_t L, uint32_t* __restrict__ owner, uint32_t* __restrict__ first,
-                              const uint32_t* __restrict__ nchunks, const uint32_t* __restrict__ binbase, uint32_t bpg,
-                              uint32_t* __restrict__ perm) {
+// chunk_off[b] = cloc[b] + blk_pre[b / 256] (the scan begun in k_chunk_counts; chunk_off[m] =
+// the total); owner[segment] = bucket; first[t] = the bucket holding position L t (the start of
+// chunk t); and the bucket order of k_bucket_order (same grid: one thread per bucket)
+__global__ __launch_bounds__(256) void k_chunk_owner(const uint32_t* __restrict__ cloc, const uint32_t* __restrict__ blk_pre,
+                                                     uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ offsets,
+                                                     uint32_t m, uint32_t L, uint32_t* __restrict__ owner,
+                                                     uint32_t* __restrict__ first, const uint32_t* __restrict__ nchunks,
+                                                     const uint32_t* __restrict__ binbase, uint32_t bpg,
+                                                     uint32_t* __restrict__ perm) {
     __shared__ uint32_t cur[ORDER_BINS];
     if (threadIdx.x < ORDER_BINS) cur[threadIdx.x] = binbase[order_index(blockIdx.x, threadIdx.x, bpg)];
     __syncthreads();
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
-    const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
+    const uint32_t k0 = cloc[b] + blk_pre[b >> 8];
+    const uint32_t k1 = b + 1 < m ? cloc[b + 1] + blk_pre[(b + 1) >> 8] : blk_pre[(m + 255) >> 8];
+    chunk_off[b] = k0;
+    if (b + 1 == m) chunk_off[m] = k1;
     for (uint32_t k = k0; k < k1; ++k) owner[k] = b;
     const uint32_t o = offsets[b], e = offsets[b + 1];
     for (uint32_t t = (o + L - 1) / L; t * L < e; ++t) first[t] = b;
@@ -1272,12 +1309,13 @@ __global__ void k_chunk_owner(const uint32_t* __restrict__ chunk_off, const uint
     if (c <= SMALL_MAX) perm[atomicAdd(&cur[c], 1u)] = b;
 }
 
-eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offsets, uint32_t m, uint32_t L,
-                                uint32_t* owner, uint32_t* first, const uint32_t* nchunks, const uint32_t* binbase,
-                                uint32_t groups, uint32_t* perm, hipStream_t st) {
+eIcicleError launch_chunk_owner(const uint32_t* cloc, const uint32_t* blk_pre, uint32_t* chunk_off,
+                                const uint32_t* offsets, uint32_t m, uint32_t L, uint32_t* owner, uint32_t* first,
+                                const uint32_t* nchunks, const uint32_t* binbase, uint32_t groups, uint32_t* perm,
+                                hipStream_t st) {
     const uint32_t nblk = (m + 255) / 256;
-    hipLaunchKernelGGL(k_chunk_owner, dim3(nblk), dim3(256), 0, st, chunk_off, offsets, m, L, owner, first, nchunks,
-                       binbase, nblk / groups, perm);
+    hipLaunchKernelGGL(k_chunk_owner, dim3(nblk), dim3(256), 0, st, cloc, blk_pre, chunk_off, offsets, m, L, owner,
+                       first, nchunks, binbase, nblk / groups, perm);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }

@@ -115,14 +115,17 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
 size_t digits_src_bytes(uint32_t n, int split);
 eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint32_t* tmp, hipStream_t st);
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
-                                 uint32_t L, uint32_t* binhist, uint32_t groups, bool zeroed, hipStream_t st);
-eIcicleError launch_order_scan(const uint32_t* binhist, uint32_t* binbase, uint32_t m, hipStream_t st);
+                                 uint32_t L, uint32_t* binhist, uint32_t groups, bool zeroed, uint32_t* cloc,
+                                 uint32_t* blk_tot, hipStream_t st);
+eIcicleError launch_order_scan(const uint32_t* binhist, uint32_t* binbase, uint32_t m, const uint32_t* blk_tot,
+                               uint32_t* blk_pre, hipStream_t st);
 uint32_t order_words(uint32_t m);
 eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const uint32_t* ranks, size_t total,
                             const uint32_t* offsets, uint32_t* sorted, hipStream_t st);
-eIcicleError launch_chunk_owner(const uint32_t* chunk_off, const uint32_t* offsets, uint32_t m, uint32_t L,
-                                uint32_t* owner, uint32_t* first, const uint32_t* nchunks, const uint32_t* binbase,
-                                uint32_t groups, uint32_t* perm, hipStream_t st);
+eIcicleError launch_chunk_owner(const uint32_t* cloc, const uint32_t* blk_pre, uint32_t* chunk_off,
+                                const uint32_t* offsets, uint32_t m, uint32_t L, uint32_t* owner, uint32_t* first,
+                                const uint32_t* nchunks, const uint32_t* binbase, uint32_t groups, uint32_t* perm,
+                                hipStream_t st);
 eIcicleError launch_scalars_from_mont(uint8_t* s, size_t n, hipStream_t st);
 eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
 eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
@@ -789,7 +792,10 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     z.words = align_up(((size_t)P.TB + 1) * 4);
     z.order = align_up(((size_t)order_words(P.TB) + 1) * 4);
     z.perm = align_up((size_t)P.TB * 4);
-    z.tmp = align_up(scan_tmp_words(std::max(std::max(max_chunks, P.TB), order_words(P.TB))) * 4);
+    // + the chunk-count block totals and their prefixes (k_chunk_counts / k_scan_small)
+    z.tmp = align_up((scan_tmp_words(std::max(std::max(max_chunks, P.TB), order_words(P.TB))) +
+                      2 * ((size_t)P.TB / 256 + 2)) *
+                     4);
     z.owner = align_up((size_t)max_chunks * 4);
     z.first = align_up((NC / P.chunk + 2) * 4);
     z.partials = align_up((size_t)max_chunks * jac);
@@ -1037,13 +1043,19 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         } else if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) {
             return er;
         }
-        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, P.groups, psort, st)) != MBLS_SUCCESS)
-            return er;
-        if ((er = launch_order_scan(binhist, binbase, TB, st)) != MBLS_SUCCESS) return er;
-        if ((er = scan_exclusive(nchunks, chunk_off, TB, tmp, st)) != MBLS_SUCCESS) return er;
-        if (!psort && (er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
-        if ((er = launch_chunk_owner(chunk_off, offsets, TB, P.chunk, owner, first, nchunks, binbase, P.groups, perm, st)) !=
+        // chunk_off = exclusive scan of the chunk counts, spread over the three kernels below:
+        // block prefixes in k_chunk_counts (written over `counts`, no longer needed), the block
+        // totals scanned beside the order histograms, the sum in k_chunk_owner
+        uint32_t* cloc = counts;
+        uint32_t* blk_tot = tmp;
+        uint32_t* blk_pre = tmp + (TB / 256 + 2);
+        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, P.groups, psort, cloc, blk_tot, st)) !=
             MBLS_SUCCESS)
+            return er;
+        if ((er = launch_order_scan(binhist, binbase, TB, blk_tot, blk_pre, st)) != MBLS_SUCCESS) return er;
+        if (!psort && (er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_chunk_owner(cloc, blk_pre, chunk_off, offsets, TB, P.chunk, owner, first, nchunks, binbase,
+                                     P.groups, perm, st)) != MBLS_SUCCESS)
             return er;
     }
     // worst case: every contribution of a window in one bucket
