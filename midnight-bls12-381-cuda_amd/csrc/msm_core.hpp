@@ -261,6 +261,11 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
 //    (maxc = max chunks per bucket, computed on device).
 // ------------------------------------------------------------------------------------
 static constexpr int TREE_FANIN = 8;
+// grid cap of the heavy-bucket passes (grid-stride): for random inputs every pass exits at once,
+// and its workgroups only compete with k_bucket_small for dispatch
+#ifndef MBLS_HEAVY_GRID
+#define MBLS_HEAVY_GRID 1024u
+#endif
 
 template <class F>
 __global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict__ chunk_off,
@@ -1088,7 +1093,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             MBLS_TRY(hipStreamWaitEvent(ts, gev[g], 0));
             if (max_per_bucket > SMALL_MAX) {  // heavy buckets (no-op passes for random inputs)
                 for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
-                    hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN / G + 255) / 256, 1024u)),
+                    hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN / G + 255) / 256, (uint32_t)MBLS_HEAVY_GRID)),
                                        dim3(256), 0, ts, chunk_off, owner, b0, b1, max_chunks, nchunks + TB, step, partials);
                 hipLaunchKernelGGL(k_bucket_gather<F>, dim3((Bg + 255) / 256), dim3(256), 0, ts, chunk_off, b0, b1,
                                    nchunks + TB, partials, buckets);
@@ -1131,7 +1136,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             MBLS_TRY(hipEventRecord(ev[2], st));
             MBLS_TRY(hipStreamWaitEvent(side, ev[2], 0));
             for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
-                hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN + 255) / 256, 1024u)), dim3(256), 0, side, chunk_off,
+                hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN + 255) / 256, (uint32_t)MBLS_HEAVY_GRID)), dim3(256), 0, side, chunk_off,
                                    owner, 0u, TB, max_chunks, nchunks + TB, step, partials);
             hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, side, chunk_off, 0u, TB,
                                nchunks + TB, partials, buckets);
