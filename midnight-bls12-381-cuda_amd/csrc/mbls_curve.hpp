@@ -49,10 +49,10 @@ MBLS_DEV Jacobian<F> jac_dbl(const Jacobian<F>& p) {
     F C = sqr(B);
     F D;
     if constexpr (SqrCheaper<F>::value)
-        D = dbl(sqr(p.x + B) - A - C);  // 2((X + B)^2 - A - C) = 4 X B
+        D = dbl(sqr(add_in(p.x, B)) - A - C);  // 2((X + B)^2 - A - C) = 4 X B
     else
         D = dbl(dbl(p.x * B));
-    F E = dbl(A) + A;
+    F E = add_in(x2_in(A), A);  // 3A: feeds the products E^2 and E (D - X3) only
     F Fv = sqr(E);
     Jacobian<F> r;
     r.x = Fv - dbl(D);
@@ -81,15 +81,16 @@ MBLS_DEV Jacobian<F> jac_add(const Jacobian<F>& p, const Jacobian<F>& q) {
         if (R.is_zero()) return jac_dbl(p);
         return Jacobian<F>::inf();
     }
-    F I = sqr(dbl(H));
+    // 2H, 2R and Z1 + Z2 feed products only: unreduced operands (add_in, mbls_field.hpp)
+    F I = sqr(x2_in(H));
     F J = H * I;
-    R = dbl(R);
+    R = x2_in(R);
     F V = U1 * I;
     Jacobian<F> r;
     r.x = sqr(R) - J - dbl(V);
     r.y = mul_sum(R, V - r.x, neg(dbl(S1)), J);
     if constexpr (SqrCheaper<F>::value)
-        r.z = (sqr(p.z + q.z) - Z1Z1 - Z2Z2) * H;  // 2 Z1 Z2 H
+        r.z = (sqr(add_in(p.z, q.z)) - Z1Z1 - Z2Z2) * H;  // 2 Z1 Z2 H
     else
         r.z = dbl((p.z * q.z) * H);
     return r;
@@ -110,14 +111,15 @@ MBLS_DEV Jacobian<F> jac_madd(const Jacobian<F>& p, const Affine<F>& q) {
         return Jacobian<F>::inf();
     }
     F HH = sqr(H);
-    F I = dbl(dbl(HH));
+    // 4HH, 2R and Z1 + H feed products only: unreduced operands (add_in, mbls_field.hpp)
+    F I = x4_in(HH);
     F J = H * I;
-    R = dbl(R);
+    R = x2_in(R);
     F V = p.x * I;
     Jacobian<F> r;
     r.x = sqr(R) - J - dbl(V);
     r.y = mul_sum(R, V - r.x, neg(dbl(p.y)), J);
-    r.z = sqr(p.z + H) - Z1Z1 - HH;
+    r.z = sqr(add_in(p.z, H)) - Z1Z1 - HH;
     return r;
 }
 
@@ -131,9 +133,9 @@ MBLS_DEV bool jac_mmadd(const Jacobian<F>& p, const Affine<F>& q, Jacobian<F>& r
     const F H = q.x - p.x;
     if (H.is_zero()) return false;
     const F HH = sqr(H);
-    const F I = dbl(dbl(HH));
+    const F I = x4_in(HH);
     const F J = H * I;
-    const F R = dbl(q.y - p.y);
+    const F R = x2_in(q.y - p.y);
     const F V = p.x * I;
     r.x = sqr(R) - J - dbl(V);
     r.y = mul_sum(R, V - r.x, neg(dbl(p.y)), J);

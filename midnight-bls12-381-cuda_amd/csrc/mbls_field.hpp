@@ -92,6 +92,30 @@ struct Fp {
 using Fr = Fp<FrCfg>;
 using Fq = Fp<FqCfg>;
 
+// raw forms for Fq (see add_in above): a, b canonical (or the stated bounds) -> no reduction
+static_assert(FqCfg::MOD[11] < (1u << 29), "Fq raw operand bounds assume p < 2^381");
+MBLS_DEV Fq add_in(const Fq& a, const Fq& b) {
+    Fq r;
+    unsigned carry = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r.v[i] = __builtin_addc(a.v[i], b.v[i], carry, &carry);
+    return r;
+}
+MBLS_DEV Fq x2_in(const Fq& a) {
+    Fq r;
+    r.v[0] = a.v[0] << 1;
+#pragma unroll
+    for (int i = 1; i < 12; ++i) r.v[i] = __builtin_amdgcn_alignbit(a.v[i], a.v[i - 1], 31);
+    return r;
+}
+MBLS_DEV Fq x4_in(const Fq& a) {
+    Fq r;
+    r.v[0] = a.v[0] << 2;
+#pragma unroll
+    for (int i = 1; i < 12; ++i) r.v[i] = __builtin_amdgcn_alignbit(a.v[i], a.v[i - 1], 30);
+    return r;
+}
+
 // Carry chains use __builtin_addc / __builtin_subc, which lower to one v_add_co/v_addc
 // (v_sub_co/v_subb) per word; the 64-bit C formulation produced ~3x the instructions
 // (v_mov + v_lshl_add_u64 per word, measured on an Fq add: 148 vs 53 VALU instructions).
@@ -148,6 +172,18 @@ template <class C>
 MBLS_DEV Fp<C> dbl(const Fp<C>& a) {
     return a + a;
 }
+
+// Unreduced sums for operands that ONLY feed products (add_in, x2_in, x4_in).  A Montgomery
+// product with a * b < m R returns < 2m and its conditional subtraction makes it canonical, and
+// the squaring wants a < 2^(32N - 1) (mbls_fips.hpp).  For Fq (p < 0.82 * 2^381) an operand up
+// to 4p with a canonical partner, or two operands up to 3p, stay inside both bounds, so these
+// skip the conditional subtraction (or two) a reduced sum costs.  Other field types reduce.
+template <class F>
+MBLS_DEV F add_in(const F& a, const F& b) { return a + b; }
+template <class F>
+MBLS_DEV F x2_in(const F& a) { return dbl(a); }
+template <class F>
+MBLS_DEV F x4_in(const F& a) { return dbl(dbl(a)); }
 
 // Montgomery product a*b*2^(-32N) mod m -- no-carry CIOS, every word step is
 // v_mad_u64_u32 + one 64-bit add.  Reference implementation; the hot paths use the
