@@ -70,9 +70,10 @@ MBLS_DEV PFq2 operator*(const PFq2& a, const PFq2& b) {
 MBLS_DEV PFq2 sqr(const PFq2& a) {
     const bool j = pairdpp::odd();
     const Fq y = partner(a.v);
-    // lane 0: (a0 + a1)(a0 - a1); lane 1: 2 a1 a0
-    const Fq r = select(j, a.v, a.v + y) * select(j, y, a.v - y);
-    return {select(j, dbl(r), r)};
+    // lane 0: (a0 + a1)(a0 - a1); lane 1: a1 (2 a0).  a0 + a1 and 2 a0 feed only the product:
+    // unreduced (< 2p against a canonical partner, mbls_field.hpp add_in), and the product's own
+    // conditional subtraction leaves both lanes canonical
+    return {select(j, a.v, add_in(a.v, y)) * select(j, x2_in(y), a.v - y)};
 }
 
 MBLS_DEV PFq2 inv(const PFq2& a) {
