@@ -108,6 +108,14 @@ MBLS_DEV Fq x2_in(const Fq& a) {
     for (int i = 1; i < 12; ++i) r.v[i] = __builtin_amdgcn_alignbit(a.v[i], a.v[i - 1], 31);
     return r;
 }
+// p - a for canonical a: in (0, p], congruent to -a (an operand of a product only)
+MBLS_DEV Fq neg_in(const Fq& a) {
+    Fq r;
+    unsigned borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r.v[i] = __builtin_subc(FqCfg::MOD[i], a.v[i], borrow, &borrow);
+    return r;
+}
 MBLS_DEV Fq x4_in(const Fq& a) {
     Fq r;
     r.v[0] = a.v[0] << 2;

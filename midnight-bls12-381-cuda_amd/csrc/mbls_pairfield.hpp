@@ -63,8 +63,9 @@ MBLS_DEV PFq2 operator*(const PFq2& a, const PFq2& b) {
     const bool j = pairdpp::odd();
     const Fq y = partner(a.v);   // a_(1-j)
     const Fq bp = partner(b.v);  // b_(1-j)
-    // lane 0: a0*b0 + a1*(-b1); lane 1: a1*b0 + a0*b1
-    return {fips::mul2(a.v, select(j, bp, b.v), y, select(j, b.v, neg(bp)))};
+    // lane 0: a0*b0 + a1*(-b1); lane 1: a1*b0 + a0*b1 (-b1 as p - b1, unreduced: the lazy sum stays
+    // below 2p^2)
+    return {fips::mul2(a.v, select(j, bp, b.v), y, select(j, b.v, neg_in(bp)))};
 }
 
 MBLS_DEV PFq2 sqr(const PFq2& a) {
