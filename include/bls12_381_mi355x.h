@@ -248,6 +248,45 @@ eIcicleError mbls_g2_sum_jacobian(const mbls_g2_projective_t* points_device, int
 eIcicleError mbls_g1_jacobian_to_icicle(mbls_g1_projective_t* points_device, int count, void* stream);
 eIcicleError mbls_g2_jacobian_to_icicle(mbls_g2_projective_t* points_device, int count, void* stream);
 
+/* Scratch ownership.  Device scratch comes from a small per-device pool of contexts (arena +
+ * side streams) LEASED per call, never keyed by the caller's stream: the reference's async
+ * MSM creates a stream per call and destroys it afterwards (core/msm.rs:742, stream.rs:189),
+ * and the reference itself allocates and frees scratch inside every call
+ * (msm_kernels.cu:705-719, :872-902).  Here a context's arena grows to the high-water mark and
+ * is reused by later calls on any stream; no hipMalloc happens once it is large enough.
+ *   mbls_release_stream: the stream is about to be destroyed (ICICLE DeviceAPI
+ *     destroy_stream calls it): forget it as a context's last stream, so a new stream that
+ *     reuses the handle value is never taken to be ordered after the old one's work.
+ *   mbls_release_scratch: free the arenas of all idle contexts (after their last work).
+ *   mbls_scratch_stats: library hipMalloc / hipFree counts of scratch arenas, bytes held,
+ *     number of pool contexts (any pointer may be NULL). */
+eIcicleError mbls_release_stream(void* stream);
+eIcicleError mbls_release_scratch(void);
+void mbls_scratch_stats(uint64_t* mallocs, uint64_t* frees, uint64_t* bytes, int* contexts);
+
+/* Multi-device G1 MSM for a single-process caller (SURVEY.md section 8e in one process; the
+ * reference's Rust core binds one device per process, core/config.rs:529-531, core/msm.rs:284).
+ * Shard k = points [k*n/ndev, (k+1)*n/ndev) runs on device devs[k] against bases_per_dev[k]
+ * (that shard's bases, resident on devs[k]; flags as config->are_points_*); `scalars` holds all
+ * n scalars, on the host or on device devs[0] per config->are_scalars_on_device.  Each shard
+ * leaves its Jacobian partial sum on its device, the partials (144 B each) are copied peer to
+ * peer to devs[0], summed there and normalised once to ICICLE's (x, y, 1).  devs may repeat a
+ * device (shards then run one after another on it).  `result`: host or device (devs[0]) per
+ * config->are_results_on_device.  config->stream, if set, is a stream of devs[0]; the other
+ * shards use library streams forked from it.  batch_size must be 1 and precompute_factor 1.
+ * Concurrent multi-device calls from several host threads serialise (one library lock). */
+eIcicleError mbls_g1_msm_multi_device(const mbls_fr_t* scalars, const mbls_g1_affine_t* const* bases_per_dev,
+                                      const int* devs, int ndev, int msm_size, const MSMConfig* config,
+                                      mbls_g1_projective_t* result);
+/* the same for G2 (288-byte partials) */
+eIcicleError mbls_g2_msm_multi_device(const mbls_fr_t* scalars, const mbls_g2_affine_t* const* bases_per_dev,
+                                      const int* devs, int ndev, int msm_size, const MSMConfig* config,
+                                      mbls_g2_projective_t* result);
+
+/* ICICLE vector_sum with the staged semantics of the other vecops (host or device input,
+ * batch_size sums of `size` elements, row-major batches; result host or device). */
+eIcicleError bls12_381_vector_sum(const mbls_fr_t* a, size_t size, const VecOpsConfig* config, mbls_fr_t* output);
+
 /* Stage profiler (tracing): hipEvent pairs recorded on the caller's
  * stream around each pipeline stage ("msm.accumulate", "ntt.pass", ...) when enabled
  * (or MBLS_PROFILE=1).  read() synchronises the recorded events and returns, per stage,

@@ -74,6 +74,8 @@ EXPORTED = [
     "mbls_g1_msm_jacobian", "mbls_g2_msm_jacobian",
     "mbls_g1_sum_jacobian", "mbls_g2_sum_jacobian", "mbls_g1_jacobian_to_icicle", "mbls_g2_jacobian_to_icicle",
     "mbls_profile_enable", "mbls_profile_reset", "mbls_profile_read",
+    "mbls_release_stream", "mbls_release_scratch", "mbls_scratch_stats",
+    "mbls_g1_msm_multi_device", "mbls_g2_msm_multi_device", "bls12_381_vector_sum",
 ]
 
 _LIB = None
@@ -111,6 +113,9 @@ def lib():
         "mbls_g1_msm_jacobian": [P, P, i32, P, P], "mbls_g2_msm_jacobian": [P, P, i32, P, P],
         "mbls_g2_sum_jacobian": [P, i32, P, P], "mbls_g1_jacobian_to_icicle": [P, i32, P],
         "mbls_g2_jacobian_to_icicle": [P, i32, P],
+        "mbls_release_stream": [P], "mbls_release_scratch": [],
+        "mbls_g1_msm_multi_device": [P, P, P, i32, i32, P, P], "mbls_g2_msm_multi_device": [P, P, P, i32, i32, P, P],
+        "bls12_381_vector_sum": [P, sz, P, P],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -129,6 +134,8 @@ def lib():
     L.mbls_profile_read.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                     ctypes.POINTER(ctypes.c_long), ctypes.c_int]
     L.mbls_profile_read.restype = ctypes.c_int
+    L.mbls_scratch_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 3 + [ctypes.POINTER(ctypes.c_int)]
+    L.mbls_scratch_stats.restype = None
     _LIB = L
     return L
 
@@ -237,6 +244,17 @@ def vec_sum(x, out=None, stream=None):
     return out
 
 
+def vector_sum(a, batch=1, out=None, stream=None, is_async=False):
+    """ICICLE vector_sum (bls12_381_vector_sum): `batch` row-major sums of a (batch*n, 4), host
+    numpy or device torch -> (batch, 4) numpy unless `out` is a device tensor"""
+    if out is None:
+        out = np.zeros((batch, 4), dtype=np.uint64)
+    cfg = vec_config(is_a_on_device=_is_dev(a), is_b_on_device=True, is_result_on_device=_is_dev(out),
+                     stream=stream, batch_size=batch, is_async=is_async)
+    check(lib().bls12_381_vector_sum(_p(a), a.shape[0] // batch, ctypes.byref(cfg), _p(out)), "bls12_381_vector_sum")
+    return out
+
+
 def batch_inv(x, out, stream=None):
     """element-wise inverses of device tensor x into device tensor out (may be x)"""
     cfg = vec_config(stream=stream)
@@ -324,6 +342,41 @@ def gen_scalars(out_dev, seed, montgomery=False, stream=None, start=0):
 def gen_bases(group, out_dev, seed, stream=None, start=0):
     fn = lib().mbls_gen_g1_bases_range if group == "g1" else lib().mbls_gen_g2_bases_range
     check(fn(_p(out_dev), seed, start, out_dev.shape[0], _stream_handle(stream)), "gen_bases")
+
+
+def msm_multi_device(group, scalars, bases_per_dev, devs, n, *, scalars_mont=True, points_mont=True, out=None,
+                     stream=None, is_async=False):
+    """mbls_g*_msm_multi_device: shard k of n points runs on devs[k] with bases_per_dev[k] (that
+    shard's bases, device tensors); scalars host numpy or device torch (devs[0]); ICICLE (x, y, 1)
+    result (host numpy unless `out` is a device tensor on devs[0])"""
+    nl = 18 if group == "g1" else 36
+    if out is None:
+        out = np.zeros((1, nl), dtype=np.uint64)
+    k = len(devs)
+    ptrs = (ctypes.c_void_p * k)(*[b.data_ptr() for b in bases_per_dev])
+    dv = (ctypes.c_int * k)(*devs)
+    cfg = msm_config(are_scalars_on_device=_is_dev(scalars), are_scalars_montgomery_form=scalars_mont,
+                     are_points_on_device=True, are_points_montgomery_form=points_mont,
+                     are_results_on_device=_is_dev(out), is_async=is_async, stream=stream)
+    fn = lib().mbls_g1_msm_multi_device if group == "g1" else lib().mbls_g2_msm_multi_device
+    check(fn(_p(scalars), ptrs, dv, k, n, ctypes.byref(cfg), _p(out)), f"{group} msm_multi_device")
+    return out
+
+
+def scratch_stats():
+    """(library scratch hipMallocs, hipFrees, bytes held, pool contexts)"""
+    m, f, b = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    c = ctypes.c_int()
+    lib().mbls_scratch_stats(ctypes.byref(m), ctypes.byref(f), ctypes.byref(b), ctypes.byref(c))
+    return m.value, f.value, b.value, c.value
+
+
+def release_stream(stream):
+    check(lib().mbls_release_stream(_stream_handle(stream)), "mbls_release_stream")
+
+
+def release_scratch():
+    check(lib().mbls_release_scratch(), "mbls_release_scratch")
 
 
 def sum_jacobian(group, pts_dev, out_dev, stream=None):

@@ -1,8 +1,10 @@
-// common.cpp -- error mapping, scratch arenas, configs, version.
+// common.cpp -- error mapping, the scratch-context pool, configs, version.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <string>
@@ -33,29 +35,51 @@ eIcicleError map_hip_error(hipError_t e, const char* what) {
     }
 }
 
-Arena::~Arena() {
-    // Arenas live for the process; freeing at exit races with runtime teardown, so leak.
+static std::atomic<uint64_t> g_scratch_mallocs{0}, g_scratch_frees{0}, g_scratch_bytes{0};
+void count_scratch_alloc(size_t bytes) {
+    g_scratch_mallocs.fetch_add(1);
+    g_scratch_bytes.fetch_add(bytes);
+}
+void count_scratch_free(size_t bytes) {
+    g_scratch_frees.fetch_add(1);
+    g_scratch_bytes.fetch_sub(bytes);
 }
 
-eIcicleError Arena::reserve(size_t bytes) {
+Arena::~Arena() {
+    // pool contexts live for the process; freeing at exit races with runtime teardown, so leak
+    // (mbls_release_scratch frees idle arenas explicitly)
+}
+
+eIcicleError Arena::reserve(size_t bytes, hipEvent_t idle) {
     bytes = align_up(bytes);
     if (bytes <= cap_) return MBLS_SUCCESS;
     size_t ncap = bytes + bytes / 4;
-    void* p = nullptr;
     if (base_) {
-        // older work on this stream may still read the old block: free it in stream order
-        hipError_t e = hipStreamSynchronize(stream_);
-        if (e != hipSuccess) return map_hip_error(e, "arena sync");
-        (void)hipFree(base_);
-        base_ = nullptr;
-        cap_ = 0;
+        // earlier calls of this context may still read the old block: wait for them
+        if (idle) {
+            hipError_t e = hipEventSynchronize(idle);
+            if (e != hipSuccess) return map_hip_error(e, "arena idle sync");
+        }
+        release();
     }
+    void* p = nullptr;
     hipError_t e = hipMalloc(&p, ncap);
     if (e != hipSuccess) return map_hip_error(e, "arena hipMalloc");
+    count_scratch_alloc(ncap);
     base_ = p;
     cap_ = ncap;
     used_ = 0;
     return MBLS_SUCCESS;
+}
+
+void Arena::release() {
+    if (base_) {
+        (void)hipFree(base_);
+        count_scratch_free(cap_);
+    }
+    base_ = nullptr;
+    cap_ = 0;
+    used_ = 0;
 }
 
 void* Arena::take(size_t bytes) {
@@ -66,16 +90,95 @@ void* Arena::take(size_t bytes) {
     return p;
 }
 
-StreamCtx& stream_ctx(hipStream_t s) {
-    static std::mutex g;
-    static std::map<std::pair<int, hipStream_t>, std::unique_ptr<StreamCtx>> tab;
+// ---- per-device pool of scratch contexts ------------------------------------------------
+// Lease policy (CtxLease): among the free contexts of the current device take, in order,
+//   1. one whose last call was on this same stream (stream order already serialises it);
+//   2. an idle one (its `done` event complete, or never used), the largest arena first;
+//   3. a new context while the pool holds fewer than MBLS_SCRATCH_CONTEXTS (default 4);
+//   4. the least recently used one, with the caller's stream made to wait for its `done`.
+// If every context is leased by another thread and the pool is full, wait for a release.
+struct Pool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<int, std::vector<std::unique_ptr<StreamCtx>>> by_dev;
+    uint64_t clock = 0;
+};
+static Pool& pool() {
+    static Pool* p = new Pool();  // never destroyed (see Arena::~Arena)
+    return *p;
+}
+static size_t pool_limit() {
+    static const size_t v = [] {
+        const char* e = getenv("MBLS_SCRATCH_CONTEXTS");
+        const long k = e ? atol(e) : 4;
+        return (size_t)(k > 0 ? k : 1);
+    }();
+    return v;
+}
+
+CtxLease::CtxLease(hipStream_t st) : st_(st) {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(g);
-    auto key = std::make_pair(dev, s);
-    auto it = tab.find(key);
-    if (it == tab.end()) it = tab.emplace(key, std::unique_ptr<StreamCtx>(new StreamCtx(s))).first;
-    return *it->second;
+    Pool& P = pool();
+    std::unique_lock<std::mutex> lk(P.mu);
+    auto& v = P.by_dev[dev];
+    StreamCtx* pick = nullptr;
+    bool wait = false;
+    while (!pick) {
+        StreamCtx* idle = nullptr;
+        StreamCtx* lru = nullptr;
+        for (auto& c : v) {
+            if (c->busy) continue;
+            if (c->last == st && c->used) {
+                pick = c.get();
+                break;
+            }
+            const bool is_idle = !c->used || hipEventQuery(c->done) == hipSuccess;
+            if (is_idle && (!idle || c->arena.capacity() > idle->arena.capacity())) idle = c.get();
+            if (!lru || c->stamp < lru->stamp) lru = c.get();
+        }
+        if (pick) break;
+        if (idle) {
+            pick = idle;
+        } else if (v.size() < pool_limit()) {
+            std::unique_ptr<StreamCtx> c(new StreamCtx());
+            c->device = dev;
+            if (hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
+                err_ = MBLS_UNKNOWN_ERROR;
+                return;
+            }
+            pick = c.get();
+            v.push_back(std::move(c));
+        } else if (lru) {
+            pick = lru;
+            wait = true;
+        } else {
+            P.cv.wait(lk);  // all leased by other threads
+        }
+    }
+    pick->busy = true;
+    pick->stamp = ++P.clock;
+    lk.unlock();
+    if (wait && hipStreamWaitEvent(st, pick->done, 0) != hipSuccess) {
+        err_ = MBLS_UNKNOWN_ERROR;
+        std::lock_guard<std::mutex> g(P.mu);
+        pick->busy = false;
+        P.cv.notify_one();
+        return;
+    }
+    ctx_ = pick;
+}
+
+CtxLease::~CtxLease() {
+    if (!ctx_) return;
+    // everything the call enqueued (side streams joined back) is ordered before `done`
+    const bool rec = hipEventRecord(ctx_->done, st_) == hipSuccess;
+    Pool& P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    if (rec) ctx_->used = true;
+    ctx_->last = st_;
+    ctx_->busy = false;
+    P.cv.notify_one();
 }
 
 static bool side_priority() {
@@ -101,16 +204,6 @@ eIcicleError StreamCtx::ensure_side(size_t nevents, size_t nsides) {
         MBLS_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         events.push_back(e);
     }
-    return MBLS_SUCCESS;
-}
-
-eIcicleError StreamCtx::ensure_pipe() {
-    for (int k = 0; k < 2; ++k)
-        if (!pipe[k]) MBLS_TRY(hipStreamCreateWithFlags(&pipe[k], hipStreamNonBlocking));
-    for (int k = 0; k < 3; ++k)
-        if (!pipe_ev[k]) MBLS_TRY(hipEventCreateWithFlags(&pipe_ev[k], hipEventDisableTiming));
-    for (int k = 0; k < 2; ++k)
-        if (!acc_ev[k]) MBLS_TRY(hipEventCreateWithFlags(&acc_ev[k], hipEventDisableTiming));
     return MBLS_SUCCESS;
 }
 
@@ -188,6 +281,52 @@ int mbls_profile_read(const char** names, double* total_ms, long* counts, int ma
         ++i;
     }
     return (int)mbls::g_prof_sum.size();
+}
+
+/* scratch pool (include/bls12_381_mi355x.h) */
+eIcicleError mbls_release_stream(void* stream) {
+    mbls::Pool& P = mbls::pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    for (auto& kv : P.by_dev)
+        for (auto& c : kv.second)
+            if (c->last == static_cast<hipStream_t>(stream)) c->last = nullptr;
+    return MBLS_SUCCESS;
+}
+
+eIcicleError mbls_release_scratch(void) {
+    mbls::Pool& P = mbls::pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    eIcicleError r = MBLS_SUCCESS;
+    for (auto& kv : P.by_dev)
+        for (auto& c : kv.second) {
+            if (c->busy || !c->arena.capacity()) continue;
+            if (hipSetDevice(c->device) != hipSuccess) {
+                r = MBLS_INVALID_DEVICE;
+                continue;
+            }
+            if (c->used && hipEventSynchronize(c->done) != hipSuccess) {
+                r = MBLS_SYNCHRONIZATION_FAILED;
+                continue;
+            }
+            c->arena.release();
+        }
+    (void)hipSetDevice(cur);
+    return r;
+}
+
+void mbls_scratch_stats(uint64_t* mallocs, uint64_t* frees, uint64_t* bytes, int* contexts) {
+    if (mallocs) *mallocs = mbls::g_scratch_mallocs.load();
+    if (frees) *frees = mbls::g_scratch_frees.load();
+    if (bytes) *bytes = mbls::g_scratch_bytes.load();
+    if (contexts) {
+        mbls::Pool& P = mbls::pool();
+        std::lock_guard<std::mutex> g(P.mu);
+        int k = 0;
+        for (auto& kv : P.by_dev) k += (int)kv.second.size();
+        *contexts = k;
+    }
 }
 
 const char* mbls_version(void) { return "bls12_381_mi355x 0.1 (gfx950)"; }

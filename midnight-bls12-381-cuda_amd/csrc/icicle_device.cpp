@@ -88,6 +88,10 @@ class HipDeviceAPI final : public DeviceAPI {
         return ok_or(e, eIcicleError::STREAM_CREATION_FAILED);
     }
     eIcicleError destroy_stream(icicleStreamHandle stream) const override {
+        // the library forgets the handle first (its scratch contexts are pooled per device, not
+        // per stream: nothing is freed or leaked here, and a recycled handle value is not taken
+        // to be ordered after this stream's work)
+        (void)mbls_release_stream(stream);
         return ok_or(hipStreamDestroy(hs(stream)), eIcicleError::STREAM_DESTRUCTION_FAILED);
     }
     eIcicleError get_device_properties(DeviceProperties& properties) const override {

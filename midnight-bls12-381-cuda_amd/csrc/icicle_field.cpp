@@ -56,33 +56,13 @@ eIcicleError vec_impl(const Device&, const scalar_t* a, const scalar_t* b, uint6
                      reinterpret_cast<const ::VecOpsConfig*>(&config), reinterpret_cast<mbls_fr_t*>(out)));
 }
 
-// ICICLE vector_sum: one sum per batch member (row-major batches); host operands are staged.
+// ICICLE vector_sum: one sum per batch member (row-major batches); host operands are staged in
+// the library's pooled scratch (bls12_381_vector_sum), no per-call hipMalloc
 eIcicleError vec_sum_impl(const Device&, const scalar_t* a, uint64_t size, const VecOpsConfig& config, scalar_t* out) {
     if (!a || !out) return eIcicleError::INVALID_POINTER;
-    if (config.columns_batch) return eIcicleError::API_NOT_IMPLEMENTED;
-    const int batch = config.batch_size > 0 ? config.batch_size : 1;
     if (size > (uint64_t)0x7fffffff) return eIcicleError::INVALID_ARGUMENT;
-    const size_t bytes = (size_t)size * batch * sizeof(mbls_fr_t);
-    const mbls_fr_t* src = reinterpret_cast<const mbls_fr_t*>(a);
-    void* staged = nullptr;
-    hipStream_t st = static_cast<hipStream_t>(config.stream);
-    if (!config.is_a_on_device && bytes) {
-        if (hipMalloc(&staged, bytes) != hipSuccess) return eIcicleError::ALLOCATION_FAILED;
-        if (hipMemcpyAsync(staged, a, bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
-            (void)hipFree(staged);
-            return eIcicleError::COPY_FAILED;
-        }
-        src = static_cast<const mbls_fr_t*>(staged);
-    }
-    ::VecOpsConfig c = *reinterpret_cast<const ::VecOpsConfig*>(&config);
-    c.is_a_on_device = true;
-    c.batch_size = 1;
-    if (staged) c.is_async = false;  // the staging buffer is freed below
-    ::eIcicleError e = MBLS_SUCCESS;
-    for (int k = 0; k < batch && e == MBLS_SUCCESS; ++k)
-        e = vec_sum_cuda(reinterpret_cast<mbls_fr_t*>(out) + k, src + (size_t)k * size, (int)size, &c);
-    if (staged) (void)hipFree(staged);
-    return from_c(e);
+    return from_c(bls12_381_vector_sum(reinterpret_cast<const mbls_fr_t*>(a), (size_t)size,
+                                       reinterpret_cast<const ::VecOpsConfig*>(&config), reinterpret_cast<mbls_fr_t*>(out)));
 }
 
 // static registration under "CUDA" (icicle_field_api.cu:344-352 registers the same set,

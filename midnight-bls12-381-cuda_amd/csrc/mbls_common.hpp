@@ -1,6 +1,6 @@
 // mbls_common.hpp -- host-side plumbing shared by the HIP translation units:
-// error mapping, per-stream scratch arenas (no per-call hipMalloc on the hot path, unlike the
-// reference's 7 cudaMallocs per MSM, msm_kernels.cu:705-719), staging of host/device operands.
+// error mapping, the per-device pool of scratch contexts (no per-call hipMalloc on the hot path,
+// unlike the reference's 7 cudaMallocs per MSM, msm_kernels.cu:705-719), stage profiler.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -24,50 +24,80 @@ namespace mbls {
 eIcicleError map_hip_error(hipError_t e, const char* what);
 bool trace_enabled();
 
-// Device scratch arena bound to one stream.  Grows (never shrinks) to the high-water mark;
-// reuse is safe because every user enqueues its work on the same stream.
+// Device scratch arena.  Grows (never shrinks, unless trimmed) to the high-water mark of its
+// calls; it belongs to a ScratchCtx of the per-device pool, never to a caller's stream.
 class Arena {
   public:
-    explicit Arena(hipStream_t s) : stream_(s) {}
+    Arena() = default;
     ~Arena();
     // returns a device pointer to >= bytes, 256-B aligned; valid until the next reset()
     void* take(size_t bytes);
     void reset() { used_ = 0; }
     size_t mark() const { return used_; }
     void rewind(size_t m) { used_ = m; }
-    eIcicleError reserve(size_t bytes);
+    size_t capacity() const { return cap_; }
+    // grow to >= bytes; `idle` is an event after which no earlier work reads the block (null:
+    // never used), synchronised before the old block is freed
+    eIcicleError reserve(size_t bytes, hipEvent_t idle);
+    // free the block (caller guarantees no queued work reads it)
+    void release();
 
   private:
-    hipStream_t stream_;
     void* base_ = nullptr;
     size_t cap_ = 0;
     size_t used_ = 0;
-    std::vector<void*> retired_;
 };
 
-// One arena per (device, stream); the lock is held for the whole enqueue of a call so two
-// host threads on the same stream serialise, different streams run concurrently.
+// Scratch context: an arena plus the side streams / events an MSM forks from the caller's
+// stream.  Contexts live in a per-device pool and are LEASED for one call (CtxLease), not
+// keyed by the caller's hipStream_t: the reference's callers create and destroy a stream per
+// async MSM (core/msm.rs:742 -> stream.rs:189), which must neither leak an arena per stream
+// nor hipMalloc a fresh one on the hot path.  At the end of a call the lease records `done` on
+// the caller's stream; the next lease on another stream either finds the context idle (event
+// complete), or makes its stream wait for `done`.
 struct StreamCtx {
-    std::mutex mu;
+    int device = 0;
     Arena arena;
-    // side stream for latency-bound work that overlaps the main chain (MSM tree sums);
-    // forked from / joined back into the caller's stream with events, so callers see one
-    // stream-ordered operation
+    // side streams for latency-bound work that overlaps the main chain (MSM tree sums, the
+    // endomorphism table); forked from / joined back into the caller's stream with events, so
+    // callers see one stream-ordered operation
     std::vector<hipStream_t> sides;
     std::vector<hipEvent_t> events;
-    // batch pipeline: two private streams (each with its own StreamCtx / arena) that run
-    // alternate batch members, so one member's latency-bound tail overlaps the next member's
-    // accumulation; pipe_ev[0] forks them from this stream, pipe_ev[1..2] join them back
-    hipStream_t pipe[2] = {nullptr, nullptr};
-    hipEvent_t pipe_ev[3] = {nullptr, nullptr, nullptr};
-    // acc_ev[b & 1]: member b's accumulation done; member b + 1 (other stream) waits for it, so
-    // the two streams run staggered (b+1 accumulates while b runs its tail) instead of lockstep
-    hipEvent_t acc_ev[2] = {nullptr, nullptr};
-    explicit StreamCtx(hipStream_t s) : arena(s) {}
+    hipEvent_t done = nullptr;  // recorded on the caller's stream when a call's enqueue ends
+    bool used = false;          // `done` has been recorded at least once
+    hipStream_t last = nullptr; // caller stream of the last call (cleared by mbls_release_stream)
+    bool busy = false;          // leased by a thread right now
+    uint64_t stamp = 0;         // LRU order
     eIcicleError ensure_side(size_t nevents, size_t nsides = 1);
-    eIcicleError ensure_pipe();
 };
-StreamCtx& stream_ctx(hipStream_t s);
+
+// RAII lease of a pool context for one call on stream `st` (current device).
+class CtxLease {
+  public:
+    explicit CtxLease(hipStream_t st);
+    ~CtxLease();
+    CtxLease(const CtxLease&) = delete;
+    CtxLease& operator=(const CtxLease&) = delete;
+    explicit operator bool() const { return ctx_ != nullptr; }
+    eIcicleError error() const { return err_; }
+    StreamCtx& operator*() const { return *ctx_; }
+    StreamCtx* operator->() const { return ctx_; }
+    // grow the context's arena (safe against its previous calls) and reset it
+    eIcicleError reserve(size_t bytes) {
+        ctx_->arena.reset();
+        return ctx_->arena.reserve(bytes, ctx_->used ? ctx_->done : nullptr);
+    }
+
+  private:
+    StreamCtx* ctx_ = nullptr;
+    hipStream_t st_;
+    eIcicleError err_ = MBLS_SUCCESS;
+};
+
+// library-side hipMalloc / hipFree counters of the scratch pool (tests: no allocation on the
+// hot path after the first call)
+void count_scratch_alloc(size_t bytes);
+void count_scratch_free(size_t bytes);
 
 // Reserve-then-take helper: computes the total of a list of sizes first, so the arena
 // reallocates at most once per call (before any kernel of this call is enqueued).

@@ -300,14 +300,19 @@ MBLS_DEV Fp<C> inv_fermat(const Fp<C>& a) {
     return pow_words<C, C::N>(a, e);
 }
 
-// Inversion by the batched binary GCD (mbls_binv.hpp; variable time -- this path is not
-// constant-time): full-rate word operations plus ~100 small-factor word products
-// per 31 steps, where the Fermat chain above is ~570 serial Montgomery products.  The input's
-// Montgomery limbs are inverted as an integer, (aR)^-1, then one product with R^3 (= R2 * R2 in
-// Montgomery form) gives a^-1 R.  0 -> 0 (field.cuh:750-900 semantics).
+// Inversion by the batched binary GCD (mbls_binv.hpp; variable time -- used only on public
+// data: the MSM result normalisation and G2 norms; the Fr batch inversion, whose
+// inputs may be witness-derived, keeps the fixed Fermat chain, vecops.hip): full-rate word
+// operations plus ~100 small-factor word products per 30 steps, where the Fermat chain above
+// is ~570 serial Montgomery products.  The input's Montgomery limbs are inverted as an
+// integer, (aR)^-1, then one product with R^3 (= R2 * R2 in Montgomery form) gives a^-1 R.
+// The input is reduced once first (a value in [0, 2m), e.g. the non-canonical zero m, is a
+// valid input; the GCD needs 1 <= y < m).  0 -> 0 (field.cuh:750-900 semantics).
 template <class C>
-MBLS_DEV Fp<C> inv(const Fp<C>& a) {
+MBLS_DEV Fp<C> inv(const Fp<C>& a_in) {
     constexpr int N = C::N;
+    Fp<C> a = a_in;
+    reduce_once(a);
     if (a.is_zero()) return a;
     uint32_t m[N];
 #pragma unroll

@@ -5,6 +5,8 @@
 // (msm_kernels.cu:69-143), histogram (:224-256), cub ExclusiveSum / SortPairs (:748-781).
 #include <hip/hip_runtime.h>
 
+#include <map>
+
 #include "msm_core.hpp"
 
 namespace mbls {
@@ -61,7 +63,6 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     p.pts = (size_t)n * (p.split > 1 ? p.split : F);  // point indices (P_i, then the images)
     p.contributions = (size_t)n * W * p.split;
     if (p.pts >= (1u << 31)) return MBLS_INVALID_ARGUMENT;
-    p.groups = 1;
     return plan_levels(p, Wg);
 }
 
@@ -128,14 +129,6 @@ eIcicleError plan_levels(MsmPlan& p, int Wl) {
         m = mo;
     }
     return MBLS_SUCCESS;
-}
-
-// window groups: the G groups' accumulations run in turn on the main stream while each finished
-// group's tail (bucket sums, reduction, its windows' fold) runs on a side stream (msm_device)
-eIcicleError set_groups(MsmPlan& p, int G) {
-    if (G < 1 || p.Wg % G != 0 || ((size_t)(p.Wg / G) * p.B) % 256 != 0) G = 1;
-    p.groups = G;
-    return plan_levels(p, p.Wg / G);
 }
 
 // one (key, value) contribution: the histogram atomic's return value is the contribution's
@@ -1359,3 +1352,38 @@ extern "C" eIcicleError mbls_gen_scalars_range(mbls_fr_t* out_device, uint64_t s
 extern "C" eIcicleError mbls_gen_scalars(mbls_fr_t* out_device, uint64_t seed, size_t n, bool montgomery, void* stream) {
     return mbls_gen_scalars_range(out_device, seed, 0, n, montgomery, stream);
 }
+
+namespace mbls {
+
+// per-device resources of mbls_g*_msm_multi_device (msm_core.hpp msm_multi_device): one
+// non-blocking stream, one event per shard, the shards' partial slots and the first device's
+// gather slots; created on first use, kept for the process (like the scratch pool)
+std::mutex& multi_device_mutex() {
+    static std::mutex* m = new std::mutex();
+    return *m;
+}
+
+eIcicleError multi_device_res(int dev, MultiDevRes*& out) {
+    static std::map<int, MultiDevRes>* tab = new std::map<int, MultiDevRes>();
+    auto it = tab->find(dev);
+    if (it != tab->end()) {
+        out = &it->second;
+        return MBLS_SUCCESS;
+    }
+    int cur = 0;
+    MBLS_TRY(hipGetDevice(&cur));
+    MBLS_TRY(hipSetDevice(dev));
+    MultiDevRes r;
+    constexpr size_t JAC = GroupTraits<Fq2>::JAC;  // the larger point
+    hipError_t e = hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking);
+    for (int k = 0; k < MAX_SHARDS && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&r.ev[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipMalloc(&r.partials, MAX_SHARDS * JAC);
+    if (e == hipSuccess) e = hipMalloc(&r.gather, (MAX_SHARDS + 1) * JAC);
+    (void)hipSetDevice(cur);
+    if (e != hipSuccess) return map_hip_error(e, "multi-device resources");
+    out = &(*tab)[dev];
+    *out = r;
+    return MBLS_SUCCESS;
+}
+
+}  // namespace mbls

@@ -38,12 +38,6 @@
 #include "mbls_curve.hpp"
 #include "mbls_rowfield.hpp"
 #include "mbls_wavepoint.hpp"
-#include "mbls_lazy.hpp"
-#include "mbls_xyzz.hpp"
-
-#ifndef MBLS_XYZZ
-#define MBLS_XYZZ 0  // 1: k_accumulate in XYZZ coordinates (measured slower: 3.49 vs 3.15 ms at G1 2^20)
-#endif
 
 namespace mbls {
 
@@ -89,8 +83,7 @@ struct MsmPlan {
     uint32_t chunk;             // contributions per accumulation thread (accumulate_chunk)
     size_t pts;                 // distinct point indices (n, n*F, or split*n)
     size_t contributions;
-    int groups;                 // window groups pipelined across streams (set_groups; 1 = one pass)
-    int levels;                 // bucket-reduction levels (of one group's launch: Wg / groups windows)
+    int levels;                 // bucket-reduction levels
     uint32_t level_m[MAX_LEVELS];  // inputs per window at each level
     uint8_t seg_log[MAX_LEVELS];   // log2 segment length per level
     uint8_t mode[MAX_LEVELS];      // MODE_LANE / MODE_ROW / MODE_WAVE per level
@@ -105,7 +98,6 @@ struct MsmPlan {
 // endo: the split the group offers (1 none, 2 G1 GLV, 4 G2 psi); make_plan decides whether to use it
 eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo = 1);
 eIcicleError plan_levels(MsmPlan& p, int Wl);
-eIcicleError set_groups(MsmPlan& p, int G);
 // bits between consecutive multiples in a precomputed table: [P, 2^s P, 2^(2s) P, ...], s = ceil(256 / F)
 int precompute_shift(int F);
 
@@ -159,9 +151,6 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
 #ifndef MBLS_ACC_MMADD
 #define MBLS_ACC_MMADD 1
 #endif
-#ifndef MBLS_LAZY_ACC
-#define MBLS_LAZY_ACC 0  // measured slower: 35 VGPR spills at the 3-wave bound
-#endif
 template <class F, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ chunk_off,
@@ -192,40 +181,9 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
     // one point ahead: the next random 96/192-byte fetch overlaps this mixed addition
     uint32_t v = sorted[beg];
     Affine<L> p = fetch(v);
-#if MBLS_XYZZ
-    // XYZZ accumulator (mbls_xyzz.hpp); one flush site converts to the Jacobian partial
-    XYZZ<L> xa = XYZZ<L>::inf();
-    for (uint32_t e = beg;; ++e) {
-        if (e == bend || e == end) {  // bucket boundary or chunk end: flush
-            store_jac<L>(partials, seg, xyzz_to_jac(xa));
-            if (e == end) break;
-            xa = XYZZ<L>::inf();
-            do {
-                ++b;
-            } while (offsets[b + 1] == e);  // skip empty buckets
-            seg = chunk_off[b];
-            bend = offsets[b + 1];
-        }
-        const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
-        const Affine<L> pn = fetch(vn);
-        xa = xyzz_madd(xa, (v & 1) ? aff_neg(p) : p);
-        v = vn;
-        p = pn;
-    }
-    (void)acc;
-#else
-    // G1: the accumulator lives in the lazy [0, 2p) representation (mbls_lazy.hpp) and is made
-    // canonical where it is stored
-    constexpr bool LAZY = std::is_same<L, Fq>::value && MBLS_LAZY_ACC;
-    auto flush = [&](const Jacobian<L>& a) {
-        if constexpr (LAZY)
-            store_jac<L>(partials, seg, lz::canon(a));
-        else
-            store_jac<L>(partials, seg, a);
-    };
     for (uint32_t e = beg; e < end; ++e) {
         if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
-            flush(acc);
+            store_jac<L>(partials, seg, acc);
             acc = Jacobian<L>::inf();
             do {
                 ++b;
@@ -240,18 +198,12 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
         // is still the first point, Z = 1, so the affine + affine formula applies (~55% of a
         // mixed addition); a bucket boundary at this step left it at the identity instead
         bool done = false;
-        if (MBLS_ACC_MMADD && !LAZY && e == beg + 1 && !acc.is_inf() && !q.is_inf()) done = jac_mmadd(acc, q, acc);
-        if (!done) {
-            if constexpr (LAZY)
-                acc = lz::madd(acc, q);
-            else
-                acc = jac_madd(acc, q);
-        }
+        if (MBLS_ACC_MMADD && e == beg + 1 && !acc.is_inf() && !q.is_inf()) done = jac_mmadd(acc, q, acc);
+        if (!done) acc = jac_madd(acc, q);
         v = vn;
         p = pn;
     }
-    flush(acc);
-#endif
+    store_jac<L>(partials, seg, acc);
 }
 
 // ------------------------------------------------------------------------------------
@@ -527,27 +479,6 @@ __global__ void k_final(const uint8_t* __restrict__ windows, int Wg, int c, uint
     IO::st(result, 0, final_fold<F, MODE>(windows, Wg, c));
 }
 
-// window-group fold chain (msm_device, groups > 1): acc = 2^ndbl acc, then acc += H_g (acc = H_g
-// for the first group); the doublings only wait for the previous fold, not for group g's tail
-template <class F>
-__global__ void k_fold_dbl(uint8_t* __restrict__ acc, int ndbl) {
-    MBLS_TAIL_PRIO();
-    using IO = RedIO<F, MODE_WAVE>;
-    if (IO::id() != 0) return;
-    auto a = IO::ld(acc, 0);
-    for (int k = 0; k < ndbl; ++k) a = IO::dbl(a);
-    IO::st(acc, 0, a);
-}
-template <class F>
-__global__ void k_fold_add(uint8_t* __restrict__ acc, const uint8_t* __restrict__ h, int first) {
-    MBLS_TAIL_PRIO();
-    using IO = RedIO<F, MODE_WAVE>;
-    if (IO::id() != 0) return;
-    auto a = IO::ld(h, 0);
-    if (!first) a = IO::add(IO::ld(acc, 0), a);
-    IO::st(acc, 0, a);
-}
-
 template <class F>
 __global__ void k_store_inf(uint8_t* result, int count) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -733,10 +664,9 @@ struct MsmScratchSizes {
     size_t dsrc, keys, vals, ranks, sorted, words, tmp, owner, first, partials, buckets, levelT, levelR, sums, windows, treetmp, phi;
     size_t ent, segtab, parts;  // partitioned sort (keys / vals / ranks are 0 then)
     size_t order, perm;         // k_bucket_order: bin histograms / their scan, bucket permutation
-    size_t gsum;                // window groups' folds H_g
     size_t total() const {
         return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + first + partials + buckets + levelT + levelR + sums + windows +
-               2 * TREE_SIDES * treetmp + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm + gsum;
+               2 * TREE_SIDES * treetmp + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm;
     }
 };
 
@@ -748,15 +678,6 @@ inline bool defer_narrow_trees() {
         return e ? atoi(e) != 0 : true;
     }();
     return v;
-}
-
-// batch members in order on the caller's stream (default), or on two staggered pipeline streams
-// (MBLS_BATCH_PIPE=1: member b+1 accumulates while member b runs its tail).  Measured G1 2^20
-// batch 8: in order 207 MSM/s, staggered pipeline 204 (the tails' row-sliced chains slow the
-// VALU-saturated accumulation beside them about as much as they hide), unstaggered 197
-inline bool batch_pipeline() {  // read per call: the GPU tests switch it
-    const char* e = getenv("MBLS_BATCH_PIPE");
-    return e ? atoi(e) != 0 : false;
 }
 
 // reduction levels with fewer segments than this run one segment per wave (MBLS_WAVE_MIN tunes;
@@ -815,7 +736,6 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     z.levelR = align_up(lv * P.Wg * jac);
     z.sums = align_up((size_t)P.levels * P.Wg * jac);
     z.windows = align_up((size_t)P.Wg * jac);
-    z.gsum = align_up((size_t)P.groups * jac);
     z.treetmp = align_up(maxblk * P.Wg * jac);
     return z;
 }
@@ -894,71 +814,15 @@ inline void launch_reduce_level(int mode, const uint8_t* V, uint32_t m_in, uint3
                            Wl, off, T, R);
 }
 
-// bucket reduction of one window group (Wl windows, group g) on one stream: the levels, each
-// level's T sum (tree stages in line, narrow levels batched into one launch), the window Horner.
-// V = the group's buckets; level l's outputs live at [lvoff_l * Wg + g * Wl * m_out_l) of the
-// level arrays (all groups side by side); sums / windows point at the group's slices.
-template <class F>
-eIcicleError reduce_windows(const MsmPlan& P, const uint8_t* V, int Wl, int g, uint8_t* levelT, uint8_t* levelR,
-                            uint8_t* sums, uint8_t* windows, uint8_t* const (&tt)[2], hipStream_t s) {
-    constexpr size_t JAC = GroupTraits<F>::JAC;
-    size_t lvoff = 0;
-    TreeJobs jobs;
-    int njobs = 0;
-    for (int l = 0; l < P.levels; ++l) {
-        const uint32_t m_in = P.level_m[l], seg = P.seg(l);
-        const uint32_t m_out = (m_in + seg - 1) / seg;
-        const size_t at = (lvoff * P.Wg + (size_t)g * Wl * m_out) * JAC;
-        uint8_t* T = levelT + at;
-        uint8_t* R = levelR + at;
-        launch_reduce_level<F>(P.mode[l], V, m_in, seg, Wl, l == 0 ? 1 : 0, T, R, m_out * (uint32_t)Wl, s);
-        if (m_out <= TREE_DEFER_POINTS) {
-            jobs.V[njobs] = T;
-            jobs.m[njobs] = m_out;
-            jobs.out[njobs] = sums + (size_t)l * Wl * JAC;
-            ++njobs;
-        } else {
-            const uint8_t* src = T;
-            uint32_t m = m_out;
-            int flip = 0;
-            while (true) {
-                const uint32_t nblk = tree_blocks(m);
-                uint8_t* dst = nblk == 1 ? sums + (size_t)l * Wl * JAC : tt[flip];
-                hipLaunchKernelGGL(k_tree_sum<F>, dim3(Wl * nblk), dim3(256), 0, s, src, m, nblk, dst);
-                if (nblk == 1) break;
-                src = dst;
-                m = nblk;
-                flip ^= 1;
-            }
-        }
-        V = R;
-        lvoff += m_out;
-    }
-    if (njobs) hipLaunchKernelGGL(k_tree_sum_jobs<F>, dim3(njobs * Wl), dim3(256), 0, s, jobs, Wl);
-    hipLaunchKernelGGL((k_window_horner<F, MODE_WAVE>), dim3(Wl), dim3(64), 0, s, sums, P.levels, Wl, P.seg_logs_packed(),
-                       windows);
-    MBLS_TRY(hipGetLastError());
-    return MBLS_SUCCESS;
-}
-
-// window groups for one MSM (MBLS_GROUPS; default 1 = one pass over all windows).  Measured
-// at G1 2^20: 2 / 4 / 8 groups 171 / 165 / 125 MSM/s against 191 for one
-// pass -- the tails are latency-bound row / wave-sliced chains that cost ~4x the VALU issue per
-// product of the lane-sliced accumulation, so beside it they slow the accumulation (3.27 ->
-// 4.15 ms summed over 4 groups) more than they hide.
-inline int msm_groups() {  // read per call: the GPU tests switch it
-    const char* e = getenv("MBLS_GROUPS");
-    return e ? atoi(e) : 1;
-}
-
 // Core MSM on device operands: scalars (standard or Montgomery), bases Montgomery affine
-// (F*n entries when precomputed); result: one Jacobian Montgomery point on device.
-// use_side = false runs everything on `st` (pipelined batch members: their overlap comes from
-// the two pipeline streams, and fewer streams than the 4 hardware queues keeps them concurrent)
+// (F*n entries when precomputed); result: one Jacobian Montgomery point on device, or, with
+// icicle_out, ICICLE's normalised (x, y, 1) written there by the final fold's launch.
+// Everything is enqueued on `st`; side streams of the leased context are forked from it and
+// joined back, so the caller sees one stream-ordered operation.
 template <class F>
 eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t* bases, uint32_t n,
-                        const MsmPlan& P, uint8_t* result, StreamCtx& ctx, hipStream_t st, bool use_side = true,
-                        hipEvent_t acc_done = nullptr, uint8_t* icicle_out = nullptr) {
+                        const MsmPlan& P, uint8_t* result, StreamCtx& ctx, hipStream_t st,
+                        uint8_t* icicle_out = nullptr) {
     Arena& arena = ctx.arena;
     constexpr size_t JAC = GroupTraits<F>::JAC, AFF = GroupTraits<F>::AFF;
     constexpr uint32_t LN = LaneOf<F>::LANES;  // lanes per chain in the lane-mode kernels
@@ -1003,32 +867,22 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint32_t* binhist = (uint32_t*)arena.take(z.order);
     uint32_t* binbase = (uint32_t*)arena.take(z.order);
     uint32_t* perm = (uint32_t*)arena.take(z.perm);
-    uint8_t* gsum = (uint8_t*)arena.take(z.gsum);
-    if (!gsum || !tree_tmp[TREE_SIDES - 1][1] || (P.split > 1 && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
+    if (!perm || !tree_tmp[TREE_SIDES - 1][1] || (P.split > 1 && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
-    // side stream: the phi(P) table and the heavy-bucket passes overlap the main chain; the
-    // per-level tree sums of the reduction run there too.  Events [levels+1 ..) fork / join.
-    // events: [0, levels] tree forks / join, [levels + 1, +8 + TREE_SIDES) table / heavy / joins,
-    // then 2 groups + 1 for the window-group pipeline (all ensured here: `ev` must stay valid)
-    if ((er = ctx.ensure_side((size_t)P.levels + 8 + TREE_SIDES + 2 * (size_t)P.groups + 1, TREE_SIDES)) != MBLS_SUCCESS)
-        return er;
-    hipStream_t side = use_side ? ctx.sides[0] : st;
+    // side streams: the endomorphism table and the heavy-bucket passes overlap the main chain;
+    // the per-level tree sums of the reduction run there too.  events: [0, levels] tree forks /
+    // join, then [levels + 1, + 4 + TREE_SIDES) table / heavy / joins
+    if ((er = ctx.ensure_side((size_t)P.levels + 5 + TREE_SIDES, TREE_SIDES)) != MBLS_SUCCESS) return er;
+    hipStream_t side = ctx.sides[0];
     hipEvent_t* ev = ctx.events.data() + P.levels + 1;
     if (P.split > 1) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
-        // the psi table (15 Fq products per point) on the main stream before the digit pass
-        // when MBLS_PSI_SERIAL=1 (beside it, the two slow each other)
-        static const bool psi_serial = [] {
-            const char* e = getenv("MBLS_PSI_SERIAL");
-            return e && atoi(e) != 0;
-        }();
-        hipStream_t ts = (P.split == 4 && psi_serial) ? st : side;
         MBLS_TRY(hipEventRecord(ev[0], st));
-        MBLS_TRY(hipStreamWaitEvent(ts, ev[0], 0));
-        er = P.split == 2 ? launch_glv_table(bases, phi, n, ts) : launch_psi_table(bases, phi, n, ts);
+        MBLS_TRY(hipStreamWaitEvent(side, ev[0], 0));
+        er = P.split == 2 ? launch_glv_table(bases, phi, n, side) : launch_psi_table(bases, phi, n, side);
         if (er != MBLS_SUCCESS) return er;
-        MBLS_TRY(hipEventRecord(ev[1], ts));
+        MBLS_TRY(hipEventRecord(ev[1], side));
     }
     {
         ProfScope ps("msm.digits", st);
@@ -1054,71 +908,18 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         uint32_t* cloc = counts;
         uint32_t* blk_tot = tmp;
         uint32_t* blk_pre = tmp + (TB / 256 + 2);
-        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, P.groups, psort, cloc, blk_tot, st)) !=
+        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, 1u, psort, cloc, blk_tot, st)) !=
             MBLS_SUCCESS)
             return er;
         if ((er = launch_order_scan(binhist, binbase, TB, blk_tot, blk_pre, st)) != MBLS_SUCCESS) return er;
         if (!psort && (er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
         if ((er = launch_chunk_owner(cloc, blk_pre, chunk_off, offsets, TB, P.chunk, owner, first, nchunks, binbase,
-                                     P.groups, perm, st)) != MBLS_SUCCESS)
+                                     1u, perm, st)) != MBLS_SUCCESS)
             return er;
     }
     // worst case: every contribution of a window in one bucket
     const uint32_t max_per_bucket = (uint32_t)((P.pts + P.chunk - 1) / P.chunk);
     const uint32_t nsplit = P.split > 1 ? n : 0xffffffffu;
-    if (P.groups > 1 && use_side) {
-        // ---- window groups: group g's accumulation on the main stream, then its tail (bucket
-        // sums, reduction, fold of its windows) on a side stream while group g-1 accumulates;
-        // the groups' folds H_g are combined top-down on a third stream, acc = 2^(c Wpg) acc +
-        // H_g, its doublings waiting only for the previous fold.  Only the last group's tail
-        // and one fold step remain after the last accumulation.
-        const int G = P.groups, Wpg = P.Wg / G;
-        const uint32_t Bg = (uint32_t)Wpg * P.B;
-        const uint32_t gwords = order_words(TB) / (uint32_t)G;
-        const size_t gev0 = (size_t)P.levels + 8 + TREE_SIDES;
-        hipEvent_t* gev = ctx.events.data() + gev0;  // [0, G) accumulated, [G, 2G) tail done, 2G folded
-        hipStream_t comb = ctx.sides[2];
-        const uint32_t gthreads = (uint32_t)((NC / G + P.chunk - 1) / P.chunk + 2) * LN;
-        if (P.split > 1) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
-        for (int k = 0; k < G; ++k) {
-            const int g = G - 1 - k;  // top windows first: the fold is a Horner from the top
-            const uint32_t b0 = (uint32_t)g * Bg, b1 = b0 + Bg;
-            {
-                ProfScope ps("msm.accumulate", st);
-                hipLaunchKernelGGL(accumulate_kernel<F>(), dim3((gthreads + 255) / 256), dim3(256), 0, st, sorted,
-                                   offsets, chunk_off, first, b0, b1, bases, phi, nsplit, P.chunk, partials);
-            }
-            MBLS_TRY(hipEventRecord(gev[g], st));
-            hipStream_t ts = ctx.sides[k & 1];
-            MBLS_TRY(hipStreamWaitEvent(ts, gev[g], 0));
-            if (max_per_bucket > SMALL_MAX) {  // heavy buckets (no-op passes for random inputs)
-                for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
-                    hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN / G + 255) / 256, (uint32_t)MBLS_HEAVY_GRID)),
-                                       dim3(256), 0, ts, chunk_off, owner, b0, b1, max_chunks, nchunks + TB, step, partials);
-                hipLaunchKernelGGL(k_bucket_gather<F>, dim3((Bg + 255) / 256), dim3(256), 0, ts, chunk_off, b0, b1,
-                                   nchunks + TB, partials, buckets);
-            }
-            hipLaunchKernelGGL(k_bucket_small<F>, dim3((Bg * LN + 255) / 256), dim3(256), 0, ts, chunk_off, perm, binbase,
-                               (uint32_t)g, gwords, partials, buckets);
-            if ((er = reduce_windows<F>(P, buckets + (size_t)b0 * JAC, Wpg, g, levelT, levelR, sums + (size_t)g * P.levels * Wpg * JAC,
-                                        windows + (size_t)g * Wpg * JAC, tree_tmp[k & 1], ts)) != MBLS_SUCCESS)
-                return er;
-            hipLaunchKernelGGL((k_final<F, MODE_WAVE>), dim3(1), dim3(64), 0, ts, windows + (size_t)g * Wpg * JAC, Wpg, P.c,
-                               gsum + (size_t)g * JAC);
-            MBLS_TRY(hipEventRecord(gev[G + g], ts));
-            if (k > 0) hipLaunchKernelGGL(k_fold_dbl<F>, dim3(1), dim3(64), 0, comb, result, P.c * Wpg);
-            MBLS_TRY(hipStreamWaitEvent(comb, gev[G + g], 0));
-            hipLaunchKernelGGL(k_fold_add<F>, dim3(1), dim3(64), 0, comb, result, gsum + (size_t)g * JAC, k == 0 ? 1 : 0);
-        }
-        MBLS_TRY(hipEventRecord(gev[2 * G], comb));
-        {
-            ProfScope ps("msm.tail", st);  // exposed tail: last accumulation -> fold done
-            MBLS_TRY(hipStreamWaitEvent(st, gev[2 * G], 0));
-        }
-        if (icicle_out) hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3(1), dim3(64), 0, st, result, icicle_out, 1);
-        MBLS_TRY(hipGetLastError());
-        return MBLS_SUCCESS;
-    }
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
         ProfScope ps("msm.accumulate", st);
@@ -1126,7 +927,6 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         const uint32_t threads = (uint32_t)((NC + P.chunk - 1) / P.chunk) * LN;
         hipLaunchKernelGGL(accumulate_kernel<F>(), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
                            chunk_off, first, 0u, TB, bases, phi, nsplit, P.chunk, partials);
-        if (acc_done) MBLS_TRY(hipEventRecord(acc_done, st));
     }
     {
         ProfScope ps("msm.bucket_sum", st);
@@ -1136,8 +936,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             MBLS_TRY(hipEventRecord(ev[2], st));
             MBLS_TRY(hipStreamWaitEvent(side, ev[2], 0));
             for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
-                hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN + 255) / 256, (uint32_t)MBLS_HEAVY_GRID)), dim3(256), 0, side, chunk_off,
-                                   owner, 0u, TB, max_chunks, nchunks + TB, step, partials);
+                hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN + 255) / 256, (uint32_t)MBLS_HEAVY_GRID)),
+                                   dim3(256), 0, side, chunk_off, owner, 0u, TB, max_chunks, nchunks + TB, step, partials);
             hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, side, chunk_off, 0u, TB,
                                nchunks + TB, partials, buckets);
             MBLS_TRY(hipEventRecord(ev[3], side));
@@ -1148,7 +948,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     }
     ProfScope ps_red("msm.reduce", st);
     // recursive running-sum reduction.  The per-level T tree sums are latency-bound chains off
-    // the critical path: they run on the context's side stream, forked after each level and
+    // the critical path: they run on the context's side streams, forked after each level and
     // joined before the window Horner.
     const uint8_t* V = buckets;
     size_t lvoff = 0;
@@ -1164,7 +964,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         const uint32_t chains = m_out * (uint32_t)P.Wg;
         launch_reduce_level<F>(P.mode[l], V, m_in, seg, P.Wg, l == 0 ? 1 : 0, T, R, chains, st);
         // sum of this level's T per window: narrow levels are batched after the last level;
-        // wide ones run tree stages on the side stream, overlapped with the next levels
+        // wide ones run tree stages on a side stream, overlapped with the next levels
         if (m_out <= TREE_DEFER_POINTS && defer_narrow_trees()) {
             jobs.V[njobs] = T;
             jobs.m[njobs] = m_out;
@@ -1175,7 +975,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             continue;
         }
         const int sk = ntree++ % TREE_SIDES;
-        hipStream_t ts = use_side ? ctx.sides[sk] : st;
+        hipStream_t ts = ctx.sides[sk];
         used[sk] = true;
         MBLS_TRY(hipEventRecord(ctx.events[l], st));
         MBLS_TRY(hipStreamWaitEvent(ts, ctx.events[l], 0));
@@ -1199,15 +999,13 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     // join the side streams (the first also carried the table / heavy-bucket work): the others
     // fold into side 0, so the main stream waits once (each wait on it is a barrier packet,
     // ~5 us of gap ahead of the window Horner)
-    if (use_side) {
-        for (int k = 1; k < TREE_SIDES; ++k) {
-            if (!used[k]) continue;
-            MBLS_TRY(hipEventRecord(ev[3 + k], ctx.sides[k]));
-            MBLS_TRY(hipStreamWaitEvent(ctx.sides[0], ev[3 + k], 0));
-        }
-        MBLS_TRY(hipEventRecord(ctx.events[P.levels], ctx.sides[0]));
-        MBLS_TRY(hipStreamWaitEvent(st, ctx.events[P.levels], 0));
+    for (int k = 1; k < TREE_SIDES; ++k) {
+        if (!used[k]) continue;
+        MBLS_TRY(hipEventRecord(ev[3 + k], ctx.sides[k]));
+        MBLS_TRY(hipStreamWaitEvent(ctx.sides[0], ev[3 + k], 0));
     }
+    MBLS_TRY(hipEventRecord(ctx.events[P.levels], ctx.sides[0]));
+    MBLS_TRY(hipStreamWaitEvent(st, ctx.events[P.levels], 0));
     hipLaunchKernelGGL((k_window_horner<F, MODE_WAVE>), dim3(P.Wg), dim3(64), 0, st, sums, P.levels, P.Wg,
                        P.seg_logs_packed(), windows);
     {
@@ -1253,37 +1051,36 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     const size_t nbases_per = n * (size_t)P.F;
     const size_t nbases = shared ? nbases_per : nbases_per * batch;
 
-    StreamCtx& ctx = stream_ctx(st);
-    std::lock_guard<std::mutex> lk(ctx.mu);
+    CtxLease lease(st);
+    if (!lease) return lease.error();
+    StreamCtx& ctx = *lease;
     Arena& A = ctx.arena;
-    A.reset();
     size_t st_s = (!cfg->are_scalars_on_device) ? align_up(n * 32 * batch) : 0;
     size_t st_b = (!cfg->are_points_on_device || !pts_mont) ? align_up(nbases * AFF) : 0;
     size_t st_r = align_up(JAC * (size_t)batch);
     P.chunk = accumulate_chunk<F>(P);
-    // window groups pipeline one MSM's tails behind its own accumulations (side streams); the
-    // pipelined batch members already overlap each other's tails and run without side streams
-    er = set_groups(P, batch >= 2 && batch_pipeline() ? 1 : msm_groups());
-    if (er != MBLS_SUCCESS) return er;
     if (debug_enabled())
         fprintf(stderr, "[mbls] msm n=%d c=%d W=%d Wg=%d split=%d TB=%u contributions=%zu chunk=%u levels=%d\n", msm_size,
                 P.c, P.W, P.Wg, P.split, P.TB, P.contributions, P.chunk, P.levels);
     uint32_t max_chunks = (uint32_t)(P.contributions / P.chunk + P.TB + 1);
     size_t scratch = msm_scratch_sizes(P, JAC, AFF, max_chunks).total();
-    er = A.reserve(st_s + st_b + st_r + scratch + 4096);
+    er = lease.reserve(st_s + st_b + st_r + scratch + 4096);
     if (er != MBLS_SUCCESS) return er;
 
     const uint8_t* d_s = static_cast<const uint8_t*>(scalars);
     const uint8_t* d_b = static_cast<const uint8_t*>(bases);
     if (st_s) {
+        // host scalars (core/msm.rs:665,773 pass a HostSlice): the copy is stream-ordered; a
+        // pageable buffer is out of the caller's memory when hipMemcpyAsync returns, a pinned one
+        // is the caller's to keep alive until the stream completes (as in ICICLE)
         void* t = A.take(n * 32 * batch);
-        MBLS_TRY(hipMemcpyAsync(t, scalars, n * 32 * batch, hipMemcpyHostToDevice, st));
+        // hipMemcpyDefault: host memory, or another device's (mbls_g*_msm_multi_device shards)
+        MBLS_TRY(hipMemcpyAsync(t, scalars, n * 32 * batch, hipMemcpyDefault, st));
         d_s = static_cast<const uint8_t*>(t);
     }
     if (st_b) {
         void* t = A.take(nbases * AFF);
-        MBLS_TRY(hipMemcpyAsync(t, bases, nbases * AFF,
-                                cfg->are_points_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+        MBLS_TRY(hipMemcpyAsync(t, bases, nbases * AFF, hipMemcpyDefault, st));
         if (!pts_mont) {
             hipLaunchKernelGGL(k_points_to_mont<F>, dim3((unsigned)((nbases + 255) / 256)), dim3(256), 0, st,
                                (uint8_t*)t, nbases);
@@ -1292,62 +1089,122 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
         d_b = static_cast<const uint8_t*>(t);
     }
     uint8_t* d_r = static_cast<uint8_t*>(A.take(JAC * (size_t)batch));
-    if (batch >= 2 && batch_pipeline()) {
-        // members alternate between the two pipeline streams (own scratch each); member b's
-        // reduction tail runs while member b+1 accumulates on the other stream
-        if ((er = ctx.ensure_pipe()) != MBLS_SUCCESS) return er;
-        MBLS_TRY(hipEventRecord(ctx.pipe_ev[0], st));
-        for (int k = 0; k < 2; ++k) MBLS_TRY(hipStreamWaitEvent(ctx.pipe[k], ctx.pipe_ev[0], 0));
-        for (int b = 0; b < batch; ++b) {
-            hipStream_t ps = ctx.pipe[b & 1];
-            StreamCtx& pc = stream_ctx(ps);
-            std::lock_guard<std::mutex> plk(pc.mu);
-            if (b < 2) {
-                pc.arena.reset();
-                if ((er = pc.arena.reserve(scratch + 4096)) != MBLS_SUCCESS) return er;
-            }
-            pc.arena.reset();  // reuse is ordered on ps: member b-2 used it before
-            const uint8_t* sb = d_s + (size_t)b * n * 32;
-            const uint8_t* bb = d_b + (shared ? 0 : (size_t)b * nbases_per * AFF);
-            // staggered: member b starts once member b-1 has accumulated (its tail then overlaps
-            // this member's front and accumulation); without it both streams ran in lockstep
-            if (b > 0) MBLS_TRY(hipStreamWaitEvent(ps, ctx.acc_ev[(b - 1) & 1], 0));
-            er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, pc, ps, false, ctx.acc_ev[b & 1]);
-            if (er != MBLS_SUCCESS) return er;
-        }
-        for (int k = 0; k < 2; ++k) {
-            MBLS_TRY(hipEventRecord(ctx.pipe_ev[1 + k], ctx.pipe[k]));
-            MBLS_TRY(hipStreamWaitEvent(st, ctx.pipe_ev[1 + k], 0));
-        }
-    } else {
-        // one ICICLE MSM with its result on the device: the final fold writes the normalised
-        // (x, y, 1) straight into `results` (k_final_icicle; 16-byte stores, so aligned buffers only)
-        uint8_t* direct = (entry == MSM_ICICLE && batch == 1 && cfg->are_results_on_device &&
-                           ((uintptr_t)results & 15) == 0)
-                              ? (uint8_t*)results
-                              : nullptr;
-        const size_t mark = A.mark();
-        for (int b = 0; b < batch; ++b) {
-            A.rewind(mark);  // scratch reused across the batch (stream-ordered)
-            const uint8_t* sb = d_s + (size_t)b * n * 32;
-            const uint8_t* bb = d_b + (shared ? 0 : (size_t)b * nbases_per * AFF);
-            er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, ctx, st, true, nullptr, direct);
-            if (er != MBLS_SUCCESS) return er;
-        }
-        if (direct) {
+    // one ICICLE MSM with its result on the device: the final fold writes the normalised
+    // (x, y, 1) straight into `results` (k_final_icicle; 16-byte stores, so aligned buffers only)
+    uint8_t* direct = (entry == MSM_ICICLE && batch == 1 && cfg->are_results_on_device &&
+                       ((uintptr_t)results & 15) == 0)
+                          ? (uint8_t*)results
+                          : nullptr;
+    const size_t mark = A.mark();
+    for (int b = 0; b < batch; ++b) {
+        A.rewind(mark);  // scratch reused across the batch (stream-ordered)
+        const uint8_t* sb = d_s + (size_t)b * n * 32;
+        const uint8_t* bb = d_b + (shared ? 0 : (size_t)b * nbases_per * AFF);
+        er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, ctx, st, direct);
+        if (er != MBLS_SUCCESS) return er;
+    }
+    if (!direct) {
+        if (entry == MSM_ICICLE) {
+            hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch + 63) / 64), dim3(64), 0, st, d_r, d_r, batch);
             MBLS_TRY(hipGetLastError());
-            if (!cfg->is_async || st_s || (st_b && !cfg->are_points_on_device)) MBLS_TRY(hipStreamSynchronize(st));
-            return MBLS_SUCCESS;
         }
+        MBLS_TRY(hipMemcpyAsync(results, d_r, JAC * (size_t)batch,
+                                cfg->are_results_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
     }
-    if (entry == MSM_ICICLE) {
-        hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch + 63) / 64), dim3(64), 0, st, d_r, d_r, batch);
-        MBLS_TRY(hipGetLastError());
+    MBLS_TRY(hipGetLastError());
+    // is_async is honoured whatever the input placement (staged inputs live in the leased
+    // context, which later calls only reuse after this call's `done` event); a host result needs
+    // the wait
+    if (!cfg->is_async || !cfg->are_results_on_device) MBLS_TRY(hipStreamSynchronize(st));
+    return MBLS_SUCCESS;
+}
+
+// ------------------------------------------------------------------------------------
+// multi-device MSM for a single-process caller (mbls_g*_msm_multi_device): SURVEY.md 8e's
+// shard -> partial -> exchange -> EC sum -> one normalisation, with the exchange as peer copies
+// of the 144 / 288-byte Jacobian partials to the first device (RCCL's reduce ops cannot add
+// curve points; the torch.distributed path of bench.py / sharded_msm.py all-gathers them).
+// ------------------------------------------------------------------------------------
+static constexpr int MAX_SHARDS = 64;
+struct MultiDevRes {  // per device, created once, used under the multi-device lock
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[MAX_SHARDS] = {};
+    uint8_t* partials = nullptr;  // MAX_SHARDS Jacobian partials (G2 size)
+    uint8_t* gather = nullptr;    // (first device) MAX_SHARDS gathered partials + the sum
+};
+std::mutex& multi_device_mutex();
+eIcicleError multi_device_res(int dev, MultiDevRes*& out);
+
+template <class F>
+eIcicleError msm_multi_device(const void* scalars, const void* const* bases_per_dev, const int* devs, int ndev,
+                              int msm_size, const MSMConfig* cfg, void* result) {
+    constexpr size_t JAC = GroupTraits<F>::JAC;
+    if (!cfg || !result || !devs || !bases_per_dev) return MBLS_INVALID_POINTER;
+    if (ndev < 1 || ndev > MAX_SHARDS || msm_size < 0 || msm_size > (1 << MAX_MSM_LOG)) return MBLS_INVALID_ARGUMENT;
+    if (cfg->batch_size > 1 || cfg->precompute_factor > 1) return MBLS_INVALID_ARGUMENT;
+    if (msm_size > 0 && !scalars) return MBLS_INVALID_POINTER;
+    int count = 0;
+    MBLS_TRY(hipGetDeviceCount(&count));
+    for (int k = 0; k < ndev; ++k) {
+        if (devs[k] < 0 || devs[k] >= count) return MBLS_INVALID_DEVICE;
+        if (msm_size > 0 && !bases_per_dev[k]) return MBLS_INVALID_POINTER;
     }
-    MBLS_TRY(hipMemcpyAsync(results, d_r, JAC * (size_t)batch,
-                            cfg->are_results_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
-    if (!cfg->is_async || !cfg->are_results_on_device || st_s || (st_b && !cfg->are_points_on_device))
-        MBLS_TRY(hipStreamSynchronize(st));
+    int cur = 0;
+    MBLS_TRY(hipGetDevice(&cur));
+    std::lock_guard<std::mutex> lk(multi_device_mutex());
+    struct Restore {
+        int d;
+        ~Restore() { (void)hipSetDevice(d); }
+    } restore{cur};
+    const int d0 = devs[0];
+    MultiDevRes* r0 = nullptr;
+    eIcicleError er = multi_device_res(d0, r0);
+    if (er != MBLS_SUCCESS) return er;
+    hipStream_t st0 = cfg->stream ? static_cast<hipStream_t>(cfg->stream) : r0->stream;
+    // shard streams are forked from the caller's stream: the caller's earlier work on its
+    // inputs (a device scalar upload, say) is ordered before every shard
+    MBLS_TRY(hipSetDevice(d0));
+    MBLS_TRY(hipEventRecord(r0->ev[MAX_SHARDS - 1], st0));
+    const size_t n = (size_t)msm_size;
+    for (int k = 0; k < ndev; ++k) {
+        const int d = devs[k];
+        MultiDevRes* r = nullptr;
+        if ((er = multi_device_res(d, r)) != MBLS_SUCCESS) return er;
+        MBLS_TRY(hipSetDevice(d));
+        hipStream_t sk = (d == d0) ? st0 : r->stream;
+        if (sk != st0) MBLS_TRY(hipStreamWaitEvent(sk, r0->ev[MAX_SHARDS - 1], 0));
+        const size_t lo = n * (size_t)k / ndev, hi = n * (size_t)(k + 1) / ndev;
+        MSMConfig c = *cfg;
+        c.stream = sk;
+        c.batch_size = 1;
+        c.are_results_on_device = true;
+        c.is_async = true;
+        // scalars on another device than the shard's: staged (a peer copy, hipMemcpyDefault)
+        c.are_scalars_on_device = cfg->are_scalars_on_device && d == d0;
+        const uint8_t* sp = static_cast<const uint8_t*>(scalars) + lo * 32;
+        er = msm_call<F>(hi > lo ? sp : nullptr, bases_per_dev[k], (int)(hi - lo), &c, r->partials + (size_t)k * JAC,
+                         MSM_JACOBIAN);
+        if (er != MBLS_SUCCESS) return er;
+        MBLS_TRY(hipEventRecord(r->ev[k], sk));
+    }
+    // exchange: the partials to the first device, then one EC sum and one normalisation
+    MBLS_TRY(hipSetDevice(d0));
+    for (int k = 0; k < ndev; ++k) {
+        MultiDevRes* r = nullptr;
+        if ((er = multi_device_res(devs[k], r)) != MBLS_SUCCESS) return er;
+        if (devs[k] != d0) MBLS_TRY(hipStreamWaitEvent(st0, r->ev[k], 0));
+        MBLS_TRY(hipMemcpyPeerAsync(r0->gather + (size_t)k * JAC, d0, r->partials + (size_t)k * JAC, devs[k], JAC, st0));
+    }
+    uint8_t* sum = r0->gather + (size_t)MAX_SHARDS * JAC;
+    hipLaunchKernelGGL(k_sum_jac<F>, dim3(1), dim3(64), 0, st0, r0->gather, ndev, sum);
+    hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3(1), dim3(64), 0, st0, sum, sum, 1);
+    MBLS_TRY(hipGetLastError());
+    MBLS_TRY(hipMemcpyAsync(result, sum, JAC, cfg->are_results_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                            st0));
+    // the library's per-device resources are reused by the next call: it must not start before
+    // this one is done with them -- wait here unless the caller owns the first stream and the
+    // result is on the device (then the next call's shards order behind st0's event fork)
+    if (!cfg->is_async || !cfg->are_results_on_device || !cfg->stream) MBLS_TRY(hipStreamSynchronize(st0));
     return MBLS_SUCCESS;
 }
 
@@ -1366,12 +1223,11 @@ eIcicleError precompute_call(const void* in, int n, const MSMConfig* cfg, void* 
     if (factor > MAX_PRECOMPUTE) return MBLS_INVALID_ARGUMENT;
     if (n == 0) return MBLS_SUCCESS;
     hipStream_t st = static_cast<hipStream_t>(cfg->stream);
-    StreamCtx& ctx = stream_ctx(st);
-    std::lock_guard<std::mutex> lk(ctx.mu);
-    Arena& A = ctx.arena;
-    A.reset();
+    CtxLease lease(st);
+    if (!lease) return lease.error();
+    Arena& A = lease->arena;
     size_t in_b = (size_t)n * AFF, out_b = in_b * factor;
-    eIcicleError er = A.reserve(align_up(in_b) + align_up(out_b));
+    eIcicleError er = lease.reserve(align_up(in_b) + align_up(out_b));
     if (er != MBLS_SUCCESS) return er;
     uint8_t* din = (uint8_t*)A.take(in_b);
     uint8_t* dout = (uint8_t*)A.take(out_b);

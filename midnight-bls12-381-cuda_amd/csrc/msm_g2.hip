@@ -52,4 +52,10 @@ eIcicleError mbls_g2_jacobian_to_icicle(mbls_g2_projective_t* pts, int count, vo
     return MBLS_SUCCESS;
 }
 
+eIcicleError mbls_g2_msm_multi_device(const mbls_fr_t* scalars, const mbls_g2_affine_t* const* bases_per_dev, const int* devs,
+                                      int ndev, int msm_size, const MSMConfig* config, mbls_g2_projective_t* result) {
+    return msm_multi_device<G>(scalars, reinterpret_cast<const void* const*>(bases_per_dev), devs, ndev, msm_size, config,
+                               result);
+}
+
 }  // extern "C"

@@ -28,6 +28,7 @@
 
 #include <memory>
 #include <mutex>
+#include <vector>
 
 #include "mbls_common.hpp"
 #include "mbls_field.hpp"
@@ -44,19 +45,50 @@ static const uint64_t ROOT_2_32_MONT[4] = {0xb9b58d8c5f0e466aULL, 0x5b1b4c801819
                                            0x5bf3adda19e9b27bULL};
 
 // Twiddle tables of one domain build.  Callers take a shared_ptr snapshot under the lock and
-// enqueue their kernels with it; a table superseded by an extension or a release is freed only
-// when the last snapshot is dropped, after a device synchronisation, so no queued transform
-// ever reads freed memory (concurrent callers on rayon threads, SURVEY.md 8b "Threading").
+// enqueue their kernels with it, then record a use event on their stream (note_use); a table
+// superseded by an extension or a release is freed only when the last snapshot is dropped, and
+// then only after the use events of every transform that read it -- no queued transform ever
+// reads freed memory (concurrent callers on rayon threads, SURVEY.md 8b "Threading"), and no
+// device-wide synchronisation stalls unrelated work.
 struct DomainTables {
     int max_log = 0;            // stage tables built for stages 1..max_log
+    int device = 0;             // device the tables live on
     uint8_t* tw = nullptr;      // per-stage w_(2^s)^i tables (see header)
     uint8_t* tw_inv = nullptr;  // per-stage w_(2^s)^-i
-    ~DomainTables() {
-        if (tw || tw_inv) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(tw);
-            (void)hipFree(tw_inv);
+    std::mutex mu;
+    std::vector<hipEvent_t> uses;  // events after transforms that read the tables
+    // after enqueueing a transform on `st`: record a use event (completed ones are recycled)
+    void note_use(hipStream_t st) {
+        std::lock_guard<std::mutex> g(mu);
+        hipEvent_t ev = nullptr;
+        for (size_t i = 0; i < uses.size(); ++i)
+            if (hipEventQuery(uses[i]) == hipSuccess) {
+                ev = uses[i];
+                uses.erase(uses.begin() + i);
+                break;
+            }
+        if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipStreamSynchronize(st);  // no event: make the use complete instead
+            return;
         }
+        if (hipEventRecord(ev, st) != hipSuccess) {
+            (void)hipEventDestroy(ev);
+            (void)hipStreamSynchronize(st);
+            return;
+        }
+        uses.push_back(ev);
+    }
+    ~DomainTables() {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (cur != device) (void)hipSetDevice(device);
+        for (hipEvent_t ev : uses) {
+            (void)hipEventSynchronize(ev);
+            (void)hipEventDestroy(ev);
+        }
+        if (tw) (void)hipFree(tw);
+        if (tw_inv) (void)hipFree(tw_inv);
+        if (cur != device) (void)hipSetDevice(cur);
     }
 };
 
@@ -367,6 +399,7 @@ static eIcicleError build_domain(int max_log, hipStream_t st) {
     size_t count = ((size_t)1 << max_log) - 1;
     if (count == 0) count = 1;
     auto t = std::make_shared<DomainTables>();
+    MBLS_TRY(hipGetDevice(&t->device));
     MBLS_TRY(hipMalloc(&t->tw, 32 * count));
     MBLS_TRY(hipMalloc(&t->tw_inv, 32 * count));
     uint64_t w[4], wi[4];
@@ -564,15 +597,15 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
     const bool same = in_dev && out_dev && input == output;
     const bool work_in_tmp = perm_in || (coset && !inverse) || (same && !perm_out);
 
-    StreamCtx& ctx = stream_ctx(st);
-    std::lock_guard<std::mutex> lk(ctx.mu);
+    CtxLease lease(st);
+    if (!lease) return lease.error();
+    StreamCtx& ctx = *lease;
     size_t need = 0;
     if (!in_dev) need += align_up(bytes);
     if (!out_dev) need += align_up(bytes);
     if (work_in_tmp) need += align_up(bytes);
     if (perm_out) need += align_up(bytes);
-    ctx.arena.reset();
-    eIcicleError er = ctx.arena.reserve(need);
+    eIcicleError er = lease.reserve(need);
     if (er != MBLS_SUCCESS) return er;
     const uint8_t* src = reinterpret_cast<const uint8_t*>(input);
     uint8_t* dst = reinterpret_cast<uint8_t*>(output);
@@ -600,6 +633,7 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
     }
     er = ntt_device(wout, win, log_n, inverse, batch, *tables, st);
     if (er != MBLS_SUCCESS) return er;
+    tables->note_use(st);
     if (coset && inverse) {
         uint64_t gi[4];
         hfr_inv(gi, g);
@@ -610,7 +644,9 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
     if (perm_out && (er = launch_perm(dst, wout, log_n, batch, cols, out_rev, false, false, st)) != MBLS_SUCCESS)
         return er;
     if (!out_dev) MBLS_TRY(hipMemcpyAsync(output, dst, bytes, hipMemcpyDeviceToHost, st));
-    if (!cfg->is_async || !out_dev || !in_dev) MBLS_TRY(hipStreamSynchronize(st));
+    // a staged host input is out of the caller's memory once hipMemcpyAsync returns (pageable)
+    // or is the caller's to keep alive (pinned): only a host result forces the wait
+    if (!cfg->is_async || !out_dev) MBLS_TRY(hipStreamSynchronize(st));
     return MBLS_SUCCESS;
 }
 

@@ -73,9 +73,18 @@ __global__ __launch_bounds__(256) void k_sum_partial(uint8_t* __restrict__ out, 
 }
 
 // ---- batch inversion (vec_ops.cu:606-673 batch_inv_cuda): Montgomery's trick per thread
-// over a contiguous chunk, one Fermat inversion per chunk; zero inputs map to zero (field_inv
+// over a contiguous chunk, one inversion per chunk; zero inputs map to zero (field_inv
 // semantics, field.cuh:750-900).  `out` holds the prefix products between the two sweeps.
+// The inputs can be witness-derived scalars, so this path keeps the reference's constant-time
+// shape: the chunk inversion is the fixed Fermat chain a^(r-2) (field.cuh:735-900; not the
+// variable-time binary GCD of inv()), and zero inputs are handled by selects, not branches.
 static constexpr int INV_CHUNK = 64;
+MBLS_DEV Fr fr_select(bool c, const Fr& a, const Fr& b) {
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+    return r;
+}
 __global__ __launch_bounds__(256) void k_batch_inv(uint8_t* __restrict__ out, const uint8_t* __restrict__ in,
                                                    size_t n) {
     const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -86,17 +95,14 @@ __global__ __launch_bounds__(256) void k_batch_inv(uint8_t* __restrict__ out, co
     for (size_t i = s; i < e; ++i) {
         const Fr x = load<FrCfg>(in + 32 * i);
         store<FrCfg>(out + 32 * i, acc);
-        if (!x.is_zero()) acc = acc * x;
+        acc = fr_select(x.is_zero(), acc, acc * x);
     }
-    Fr inv_acc = inv(acc);
+    Fr inv_acc = inv_fermat(acc);
     for (size_t i = e; i-- > s;) {
         const Fr x = load<FrCfg>(in + 32 * i);
-        if (x.is_zero()) {
-            store<FrCfg>(out + 32 * i, Fr::zero());
-        } else {
-            store<FrCfg>(out + 32 * i, inv_acc * load<FrCfg>(out + 32 * i));
-            inv_acc = inv_acc * x;
-        }
+        const bool z = x.is_zero();
+        store<FrCfg>(out + 32 * i, fr_select(z, Fr::zero(), inv_acc * load<FrCfg>(out + 32 * i)));
+        inv_acc = fr_select(z, inv_acc, inv_acc * x);
     }
 }
 
@@ -139,15 +145,15 @@ static eIcicleError run_vec_op(const mbls_fr_t* a, const mbls_fr_t* b, size_t si
     if (total == 0) return MBLS_SUCCESS;
     const size_t bytes = total * 32;
 
-    StreamCtx& ctx = stream_ctx(st);
-    std::lock_guard<std::mutex> lk(ctx.mu);
+    CtxLease lease(st);
+    if (!lease) return lease.error();
+    StreamCtx& ctx = *lease;
     size_t need = 0;
     if (!scalar_op && !cfg->is_a_on_device) need += align_up(bytes);
     if (!cfg->is_b_on_device) need += align_up(bytes);
     if (!cfg->is_result_on_device) need += align_up(bytes);
     if (scalar_op && !cfg->is_a_on_device) need += align_up(32 * (size_t)batch);
-    ctx.arena.reset();
-    eIcicleError er = ctx.arena.reserve(need);
+    eIcicleError er = lease.reserve(need);
     if (er != MBLS_SUCCESS) return er;
 
     const uint8_t* da = reinterpret_cast<const uint8_t*>(a);
@@ -181,30 +187,43 @@ static eIcicleError run_vec_op(const mbls_fr_t* a, const mbls_fr_t* b, size_t si
         if (er != MBLS_SUCCESS) return er;
     }
     if (!cfg->is_result_on_device) MBLS_TRY(hipMemcpyAsync(output, dout, bytes, hipMemcpyDeviceToHost, st));
-    if (!cfg->is_async || !cfg->is_result_on_device || !cfg->is_a_on_device || !cfg->is_b_on_device)
-        MBLS_TRY(hipStreamSynchronize(st));
+    // staged host inputs are copied out of the caller's memory before hipMemcpyAsync returns
+    // (pageable) or are the caller's to keep alive (pinned, as in ICICLE): only a host result
+    // forces the wait
+    if (!cfg->is_async || !cfg->is_result_on_device) MBLS_TRY(hipStreamSynchronize(st));
     return MBLS_SUCCESS;
 }
 
-// sum of `size` device elements -> output (device or host per is_result_on_device)
-static eIcicleError vec_sum(mbls_fr_t* output, const mbls_fr_t* input, int size, const VecOpsConfig* cfg) {
+// sums of `batch` row-major members of `size` elements each -> output[0 .. batch) (device
+// or host per is_result_on_device); input on the host or the device per is_a_on_device
+static eIcicleError vec_sum(mbls_fr_t* output, const mbls_fr_t* input, size_t size, int batch, const VecOpsConfig* cfg) {
     if (!output || !input || !cfg) return MBLS_INVALID_POINTER;
-    if (size < 0) return MBLS_INVALID_ARGUMENT;
+    if (batch < 1) batch = 1;
     hipStream_t st = static_cast<hipStream_t>(cfg->stream);
-    StreamCtx& ctx = stream_ctx(st);
-    std::lock_guard<std::mutex> lk(ctx.mu);
-    const int blocks = size > 0 ? std::min(vec_grid((size_t)size), 1024) : 1;
-    ctx.arena.reset();
-    eIcicleError er = ctx.arena.reserve(align_up(32 * (size_t)blocks) + align_up(32));
+    CtxLease lease(st);
+    if (!lease) return lease.error();
+    StreamCtx& ctx = *lease;
+    const int blocks = size > 0 ? std::min(vec_grid(size), 1024) : 1;
+    const size_t in_bytes = 32 * size * (size_t)batch;
+    const bool stage = !cfg->is_a_on_device && in_bytes;
+    eIcicleError er = lease.reserve(align_up(32 * (size_t)blocks) + align_up(32 * (size_t)batch) +
+                                    (stage ? align_up(in_bytes) : 0));
     if (er != MBLS_SUCCESS) return er;
     uint8_t* part = static_cast<uint8_t*>(ctx.arena.take(32 * (size_t)blocks));
-    uint8_t* res = static_cast<uint8_t*>(ctx.arena.take(32));
-    hipLaunchKernelGGL(k_sum_partial, dim3(blocks), dim3(256), 0, st, part, reinterpret_cast<const uint8_t*>(input),
-                       (size_t)size);
-    hipLaunchKernelGGL(k_sum_partial, dim3(1), dim3(256), 0, st, res, part, (size_t)blocks);
+    uint8_t* res = static_cast<uint8_t*>(ctx.arena.take(32 * (size_t)batch));
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(input);
+    if (stage) {
+        void* t = ctx.arena.take(in_bytes);
+        MBLS_TRY(hipMemcpyAsync(t, input, in_bytes, hipMemcpyHostToDevice, st));
+        src = static_cast<const uint8_t*>(t);
+    }
+    for (int k = 0; k < batch; ++k) {
+        hipLaunchKernelGGL(k_sum_partial, dim3(blocks), dim3(256), 0, st, part, src + 32 * size * (size_t)k, size);
+        hipLaunchKernelGGL(k_sum_partial, dim3(1), dim3(256), 0, st, res + 32 * (size_t)k, part, (size_t)blocks);
+    }
     MBLS_TRY(hipGetLastError());
-    MBLS_TRY(hipMemcpyAsync(output, res, 32, cfg->is_result_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
-                            st));
+    MBLS_TRY(hipMemcpyAsync(output, res, 32 * (size_t)batch,
+                            cfg->is_result_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
     if (!cfg->is_async || !cfg->is_result_on_device) MBLS_TRY(hipStreamSynchronize(st));
     return MBLS_SUCCESS;
 }
@@ -218,11 +237,11 @@ static eIcicleError batch_inv(mbls_fr_t* output, const mbls_fr_t* input, int siz
     hipStream_t st = cfg ? static_cast<hipStream_t>(cfg->stream) : nullptr;
     const uint8_t* in = reinterpret_cast<const uint8_t*>(input);
     uint8_t* out = reinterpret_cast<uint8_t*>(output);
-    StreamCtx& ctx = stream_ctx(st);
-    std::lock_guard<std::mutex> lk(ctx.mu);
+    CtxLease lease(st);
+    if (!lease) return lease.error();
+    StreamCtx& ctx = *lease;
     if (in == out) {  // in place: keep a copy of the inputs for the backward sweep
-        ctx.arena.reset();
-        eIcicleError er = ctx.arena.reserve(align_up(32 * (size_t)size));
+        eIcicleError er = lease.reserve(align_up(32 * (size_t)size));
         if (er != MBLS_SUCCESS) return er;
         uint8_t* t = static_cast<uint8_t*>(ctx.arena.take(32 * (size_t)size));
         MBLS_TRY(hipMemcpyAsync(t, in, 32 * (size_t)size, hipMemcpyDeviceToDevice, st));
@@ -297,7 +316,16 @@ eIcicleError scalar_add_vec_cuda(mbls_fr_t* output, const mbls_fr_t* scalar, con
     return raw_vec_op<VecOp::ScalarAdd>(output, scalar, vec, size, config);
 }
 eIcicleError vec_sum_cuda(mbls_fr_t* output, const mbls_fr_t* input, int size, const VecOpsConfig* config) {
-    return vec_sum(output, input, size, config);
+    if (size < 0) return MBLS_INVALID_ARGUMENT;
+    if (!config) return MBLS_INVALID_POINTER;
+    VecOpsConfig c = *config;
+    c.is_a_on_device = true;  // the device-pointer entry point (vec_ops.cu:479-524)
+    return vec_sum(output, input, (size_t)size, 1, &c);
+}
+eIcicleError bls12_381_vector_sum(const mbls_fr_t* a, size_t size, const VecOpsConfig* config, mbls_fr_t* output) {
+    if (!config) return MBLS_INVALID_POINTER;
+    if (config->columns_batch) return MBLS_API_NOT_IMPLEMENTED;
+    return vec_sum(output, a, size, config->batch_size > 0 ? config->batch_size : 1, config);
 }
 eIcicleError bls12_381_batch_inv_cuda(mbls_fr_t* output, const mbls_fr_t* input, int size, const VecOpsConfig* config) {
     return batch_inv(output, input, size, config);

@@ -1,0 +1,194 @@
+"""Boundary behaviour of the HIP library under the reference's real call shapes (SURVEY.md 8b
+"Ownership" / "Threading" / "Callers"), through the C ABI, bit-exact against the oracle:
+
+* core/msm.rs:742 -> msm() -> stream.rs:189: a fresh stream per async MSM with PAGEABLE host
+  Montgomery scalars (HostSlice, core/msm.rs:665,773), device bases, the result copied back to
+  the host, the stream destroyed -- 200 times: no library hipMalloc after the first call and a
+  flat hipMemGetInfo (scratch is pooled per device, not per stream handle);
+* two host threads on two streams running MSM and NTT at once (rayon callers);
+* the single-process multi-device MSM entry (mbls_g1_msm_multi_device);
+* ICICLE vector_sum with staged host input (no per-call hipMalloc in the shim)."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+ORACLE_THREADS = 16
+
+
+@pytest.fixture(scope="module")
+def amd():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    import gpu_helpers
+    gpu_helpers.amd.lib()
+    return gpu_helpers.amd
+
+
+@pytest.fixture(scope="module")
+def gh():
+    import gpu_helpers
+    return gpu_helpers
+
+
+@pytest.fixture(scope="module")
+def hip():
+    L = ctypes.CDLL("libamdhip64.so")
+    L.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    L.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    L.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    L.hipMemGetInfo.argtypes = [ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+    return L
+
+
+def _std_scalars(seed, n, start=0):
+    s = np.zeros((start + n, 4), dtype=np.uint64)
+    H.oracle().orc_gen_scalars(H.ptr(s), seed, start + n)
+    return np.ascontiguousarray(s[start:])
+
+
+def _free_bytes(hip):
+    free, total = ctypes.c_size_t(), ctypes.c_size_t()
+    assert hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) == 0
+    return free.value
+
+
+def test_msm_per_op_stream_create_destroy_200x(amd, gh, hip):
+    """core/msm.rs:742 (ManagedStream::create) -> msm(HostSlice scalars, device bases, is_async,
+    device result) -> copy_to_host -> stream.rs:189 (destroy), 200 times at 2^16: every result
+    equals the oracle, the library makes no scratch hipMalloc after the first call, and the free
+    device memory stays flat (a per-stream arena would leak ~0.1 GB per call or hipMalloc it)"""
+    import torch
+    n, nsets = 1 << 16, 4
+    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 0x5EED0B01)
+    bn = amd.to_numpy_u64(b)
+    sets, refs = [], []
+    for k in range(nsets):
+        d = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+        amd.gen_scalars(d, 0x5EED0B10 + k, montgomery=True)
+        sets.append(np.ascontiguousarray(amd.to_numpy_u64(d)))  # pageable host Montgomery scalars
+        refs.append(H.g1_from_affine_mont(H.oracle_msm("g1", _std_scalars(0x5EED0B10 + k, n), bn,
+                                                       threads=ORACLE_THREADS)))
+    torch.cuda.synchronize()
+    dres = torch.zeros((1, 18), dtype=torch.int64, device="cuda")  # DeviceVec::device_malloc(1)
+    m0 = f0 = None
+    for it in range(200):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreateWithFlags(ctypes.byref(s), 1) == 0  # hipStreamNonBlocking
+        amd.msm("g1", sets[it % nsets], b, scalars_mont=True, out=dres, stream=s.value, is_async=True, n=n)
+        assert hip.hipStreamSynchronize(s) == 0  # copy_to_host is ordered after the MSM
+        host = amd.to_numpy_u64(dres)
+        amd.release_stream(s.value)  # what HipDeviceAPI::destroy_stream does first
+        assert hip.hipStreamDestroy(s) == 0
+        assert gh.decode_icicle("g1", host[0]) == refs[it % nsets], it
+        if it == 0:
+            torch.cuda.synchronize()
+            m0, f0 = amd.scratch_stats()[0], _free_bytes(hip)
+    mallocs, frees, held, ctxs = amd.scratch_stats()
+    assert mallocs == m0, (m0, mallocs)
+    assert abs(_free_bytes(hip) - f0) < (64 << 20)
+    assert ctxs <= 4
+
+
+def test_two_threads_msm_and_ntt_concurrent(amd, gh):
+    """two host threads, each on its own stream: one runs G1 MSMs with host scalars, the other
+    forward NTTs of device data; both interleave and both stay bit-exact (SURVEY.md 8b
+    "Threading": rayon callers with a stream per op)"""
+    import torch
+    amd.ntt_init_domain()
+    n, log_n, reps = 1 << 15, 16, 6
+    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 0x5EED0B21)
+    d = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(d, 0x5EED0B22, montgomery=True)
+    x = torch.zeros((1 << log_n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(x, 0x5EED0B23, montgomery=True)
+    torch.cuda.synchronize()
+    hs = np.ascontiguousarray(amd.to_numpy_u64(d))
+    ref_msm = H.g1_from_affine_mont(H.oracle_msm("g1", _std_scalars(0x5EED0B22, n), amd.to_numpy_u64(b),
+                                                 threads=ORACLE_THREADS))
+    ref_ntt = H.oracle_ntt(amd.to_numpy_u64(x), log_n, False, threads=ORACLE_THREADS)
+    errors, got_msm, got_ntt = [], [], []
+    ys = [torch.zeros_like(x) for _ in range(reps)]  # allocated (and zero-filled) before the threads
+    torch.cuda.synchronize()
+
+    def msm_worker():
+        try:
+            st = torch.cuda.Stream()
+            for _ in range(reps):
+                got_msm.append(gh.decode_icicle("g1", amd.msm("g1", hs, b, scalars_mont=True, stream=st, n=n)[0]))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def ntt_worker():
+        try:
+            st = torch.cuda.Stream()
+            for k in range(reps):
+                amd.ntt(x, out=ys[k], stream=st)  # synchronous on st (is_async false)
+                got_ntt.append(amd.to_numpy_u64(ys[k]))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=msm_worker), threading.Thread(target=ntt_worker)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert len(got_msm) == reps and len(got_ntt) == reps
+    assert all(g == ref_msm for g in got_msm)
+    assert all(np.array_equal(g, ref_ntt) for g in got_ntt)
+
+
+@pytest.mark.parametrize("ndev", [1, 3])
+def test_msm_multi_device_entry(amd, gh, ndev):
+    """mbls_g1_msm_multi_device (the single-process form of SURVEY.md 8e): shards of an uneven
+    split, each with its own bases buffer, on device 0 (one GPU here: the shards run in turn),
+    host and device scalars, host and device result -- equal to the oracle"""
+    import torch
+    n = (1 << 18) + 5
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0B31, montgomery=True)
+    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 0x5EED0B32)
+    torch.cuda.synchronize()
+    ref = H.g1_from_affine_mont(H.oracle_msm("g1", _std_scalars(0x5EED0B31, n), amd.to_numpy_u64(b),
+                                             threads=ORACLE_THREADS))
+    shards = [b[n * k // ndev:n * (k + 1) // ndev].clone() for k in range(ndev)]
+    torch.cuda.synchronize()
+    r = amd.msm_multi_device("g1", s, shards, [0] * ndev, n)
+    assert gh.decode_icicle("g1", r[0]) == ref
+    out = torch.zeros((1, 18), dtype=torch.int64, device="cuda")
+    amd.msm_multi_device("g1", np.ascontiguousarray(amd.to_numpy_u64(s)), shards, [0] * ndev, n, out=out)
+    torch.cuda.synchronize()
+    assert gh.decode_icicle("g1", amd.to_numpy_u64(out)[0]) == ref
+    with pytest.raises(amd.IcicleError):
+        amd.msm_multi_device("g1", s, shards, [99] * ndev, n)
+
+
+def test_vector_sum_staged_batch(amd):
+    """ICICLE vector_sum (bls12_381_vector_sum): host input staged in the pooled scratch, batch of
+    3 row-major sums, against the oracle's sums"""
+    import torch
+    n, batch = 5000, 3
+    x = torch.zeros((n * batch, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(x, 0x5EED0B41, montgomery=True)
+    torch.cuda.synchronize()
+    xn = np.ascontiguousarray(amd.to_numpy_u64(x))
+    m0 = amd.scratch_stats()[0]
+    got_host = amd.vector_sum(xn, batch=batch)
+    got_dev = amd.vector_sum(x, batch=batch)
+    for k in range(batch):
+        acc = np.zeros((1, 4), dtype=np.uint64)
+        tmp = np.zeros((1, 4), dtype=np.uint64)
+        for row in xn[k * n:(k + 1) * n]:
+            H.oracle().orc_vec_add(H.ptr(tmp), H.ptr(acc), H.ptr(np.ascontiguousarray(row.reshape(1, 4))), 1)
+            acc[:] = tmp
+        assert np.array_equal(got_host[k], acc[0]), k
+        assert np.array_equal(got_dev[k], acc[0]), k
+    assert amd.scratch_stats()[0] - m0 <= 1  # at most one arena growth, never per call

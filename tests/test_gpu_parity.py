@@ -615,41 +615,6 @@ def test_bench_ntt_2_22_single_and_batch4(amd):
     assert torch.equal(z, x)
 
 
-@pytest.mark.parametrize("env", [{"MBLS_GROUPS": "2"}, {"MBLS_GROUPS": "4"}, {"MBLS_GROUPS": "8"},
-                                 {"MBLS_BATCH_PIPE": "1"}])
-def test_msm_optional_schedules(amd, gh, env):
-    """the non-default schedules (msm_core.hpp): window groups pipelined over side streams
-    (MBLS_GROUPS) and the staggered two-stream batch pipeline (MBLS_BATCH_PIPE) give the oracle's
-    sums -- G1 with c = 16 (8 GLV windows: groups of 4 / 2 / 1), G2 (4 psi windows), batch of 3"""
-    import os
-    import torch
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        for group, n, w in (("g1", 3000, 12), ("g2", 700, 24)):
-            s = torch.zeros((3 * n, 4), dtype=torch.int64, device="cuda")
-            amd.gen_scalars(s, 0x5EED00D1, montgomery=True)
-            b = torch.zeros((n, w), dtype=torch.int64, device="cuda")
-            amd.gen_bases(group, b, 0x5EED00D2)
-            out = torch.zeros((3, w * 3 // 2), dtype=torch.int64, device="cuda")
-            amd.msm(group, s, b, scalars_mont=True, c=16, batch=3, out=out, n=n)
-            torch.cuda.synchronize()
-            dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
-            for k in range(3):
-                ref = H.oracle_msm(group, _oracle_std_scalars(0x5EED00D1, n, start=k * n), amd.to_numpy_u64(b))
-                assert gh.decode_icicle(group, amd.to_numpy_u64(out)[k]) == dec(ref), (group, k)
-            one = torch.zeros((1, w * 3 // 2), dtype=torch.int64, device="cuda")
-            amd.msm(group, s[:n], b, scalars_mont=True, c=16, out=one, n=n)
-            torch.cuda.synchronize()
-            assert torch.equal(one[0], out[0]), group
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
 @pytest.mark.parametrize("log_n", [21, 22])
 def test_msm_g1_chunk_scaling_sizes(amd, gh, log_n):
     """the accumulation chunk scales with the bucket size (16 at 2^21, 32 at 2^22, 128 at 2^24:
@@ -672,7 +637,8 @@ def test_msm_g1_chunk_scaling_sizes(amd, gh, log_n):
 @pytest.mark.slow
 def test_msm_g1_2_24_single_and_sharded(amd, gh):
     """north-star size (BASELINE config #4): G1 MSM of 2^24 points (scalars 0x5EED0004, bases
-    0x5EED0013) on one GPU through the ICICLE entry, and the bench's sharded sequence for 8
+    0x5EED0013) on one GPU through the ICICLE entry, the C-ABI multi-device entry with 8 shards
+    on this GPU (mbls_g1_msm_multi_device), and the bench's sharded sequence for 8
     ranks -- each shard of 2^21 generated from its slice of the global streams, one Jacobian
     partial per shard (mbls_g1_msm_jacobian), partials stacked as the all-gather would, summed
     (mbls_g1_sum_jacobian) and normalised once (mbls_g1_jacobian_to_icicle) -- both equal to
@@ -688,8 +654,12 @@ def test_msm_g1_2_24_single_and_sharded(amd, gh):
     amd.msm("g1", s, b, scalars_mont=True, out=out)
     torch.cuda.synchronize()
     single = gh.decode_icicle("g1", amd.to_numpy_u64(out)[0])
+    # the single-process multi-device entry with the shard loop forced to 8 shards on this GPU
+    # (mbls_g1_msm_multi_device, devs = [0] * 8; each shard's bases are its slice of the table)
+    shard_b = [b[sharded_msm.shard_range(n, world, r)[0]:sharded_msm.shard_range(n, world, r)[1]] for r in range(world)]
+    multi = gh.decode_icicle("g1", amd.msm_multi_device("g1", s, shard_b, [0] * world, n)[0])
     bn = amd.to_numpy_u64(b)
-    del s, b
+    del s, b, shard_b
     parts = torch.zeros((world, 18), dtype=torch.int64, device="cuda")
     for r in range(world):
         lo, hi = sharded_msm.shard_range(n, world, r)
@@ -706,3 +676,4 @@ def test_msm_g1_2_24_single_and_sharded(amd, gh):
     ref = H.g1_from_affine_mont(H.oracle_msm("g1", _oracle_std_scalars(0x5EED0004, n), bn, threads=ORACLE_THREADS))
     assert single == ref
     assert sharded == ref
+    assert multi == ref
