@@ -39,6 +39,12 @@ template <class F>
 struct SqrCheaper {
     static constexpr bool value = true;
 };
+// x2_in / x4_in / x8_in are free-standing shifts (no reduction) and a square costs a full
+// product: G1 rows (mbls_rowfield.hpp specialises this for RFq)
+template <class F>
+struct ShiftOperands {
+    static constexpr bool value = false;
+};
 
 template <class F>
 MBLS_DEV Jacobian<F> jac_dbl(const Jacobian<F>& p) {
@@ -46,19 +52,29 @@ MBLS_DEV Jacobian<F> jac_dbl(const Jacobian<F>& p) {
     if (p.is_inf()) return p;
     F A = sqr(p.x);
     F B = sqr(p.y);
-    F C = sqr(B);
-    F D;
-    if constexpr (SqrCheaper<F>::value)
-        D = dbl(sqr(add_in(p.x, B)) - A - C);  // 2((X + B)^2 - A - C) = 4 X B
-    else
-        D = dbl(dbl(p.x * B));
     F E = add_in(x2_in(A), A);  // 3A: feeds the products E^2 and E (D - X3) only
     F Fv = sqr(E);
     Jacobian<F> r;
-    r.x = Fv - dbl(D);
-    F C8 = dbl(dbl(dbl(C)));
-    r.y = E * (D - r.x) - C8;
-    r.z = dbl(p.y * p.z);
+    if constexpr (SqrCheaper<F>::value) {
+        F C = sqr(B);
+        F D = dbl(sqr(add_in(p.x, B)) - A - C);  // 2((X + B)^2 - A - C) = 4 X B
+        r.x = Fv - dbl(D);
+        F C8 = dbl(dbl(dbl(C)));
+        r.y = E * (D - r.x) - C8;
+        r.z = dbl(p.y * p.z);
+    } else {
+        // row types: a square is a full product, and the constant factors ride on unreduced
+        // operands (x4_in, x8_in, x2_in: shifts) instead of reduced doublings of the results
+        F D = x4_in(p.x) * B;  // 4 X B
+        F C8;                  // 8 C = 8 B^2
+        if constexpr (ShiftOperands<F>::value)
+            C8 = x8_in(B) * B;
+        else
+            C8 = dbl(dbl(dbl(sqr(B))));  // Fq2: a square is 2 Fq products, a product 3
+        r.x = Fv - dbl(D);
+        r.y = E * (D - r.x) - C8;
+        r.z = x2_in(p.y) * p.z;  // 2 Y Z
+    }
     return r;
 }
 
@@ -88,11 +104,13 @@ MBLS_DEV Jacobian<F> jac_add(const Jacobian<F>& p, const Jacobian<F>& q) {
     F V = U1 * I;
     Jacobian<F> r;
     r.x = sqr(R) - J - dbl(V);
-    r.y = mul_sum(R, V - r.x, neg(dbl(S1)), J);
-    if constexpr (SqrCheaper<F>::value)
+    if constexpr (SqrCheaper<F>::value) {
+        r.y = mul_sum(R, V - r.x, neg(dbl(S1)), J);
         r.z = (sqr(add_in(p.z, q.z)) - Z1Z1 - Z2Z2) * H;  // 2 Z1 Z2 H
-    else
-        r.z = dbl((p.z * q.z) * H);
+    } else {
+        r.y = R * (V - r.x) - x2_in(S1) * J;  // row types: one subtraction, 2 S1 as a shift
+        r.z = x2_in(p.z * q.z) * H;
+    }
     return r;
 }
 

@@ -192,6 +192,8 @@ template <class F>
 MBLS_DEV F x2_in(const F& a) { return dbl(a); }
 template <class F>
 MBLS_DEV F x4_in(const F& a) { return dbl(dbl(a)); }
+template <class F>
+MBLS_DEV F x8_in(const F& a) { return dbl(dbl(dbl(a))); }
 
 // Montgomery product a*b*2^(-32N) mod m -- no-carry CIOS, every word step is
 // v_mad_u64_u32 + one 64-bit add.  Reference implementation; the hot paths use the

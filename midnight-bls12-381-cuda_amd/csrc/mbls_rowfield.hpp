@@ -171,6 +171,26 @@ MBLS_DEV RFq operator-(const RFq& a, const RFq& b) {
 MBLS_DEV RFq neg(const RFq& a) { return RFq::zero() - a; }
 MBLS_DEV RFq dbl(const RFq& a) { return a + a; }
 
+// Unreduced operands for row products (the row counterparts of mbls_field.hpp's add_in / x2_in /
+// x4_in): the row CIOS product returns < 2p, and its own conditional subtraction makes it
+// canonical, whenever a * b < p * 2^384 -- e.g. an operand up to 8p against a canonical one
+// (p < 2^381).  A shift by k is one row DPP move plus one v_alignbit per lane (no carry
+// lookahead, no conditional subtraction): valid for a < 2^(384 - k), which also keeps the
+// padding lane 12 zero.  add_in keeps the lookahead but skips the conditional subtraction.
+template <int K>
+MBLS_DEV RFq rf_shl(const RFq& a) {
+    return {__builtin_amdgcn_alignbit(a.v, rowdpp::from_down(a.v), 32 - K)};
+}
+MBLS_DEV RFq x2_in(const RFq& a) { return rf_shl<1>(a); }
+MBLS_DEV RFq x4_in(const RFq& a) { return rf_shl<2>(a); }
+MBLS_DEV RFq x8_in(const RFq& a) { return rf_shl<3>(a); }
+MBLS_DEV RFq add_in(const RFq& a, const RFq& b) {  // a + b < 2^384, no reduction
+    uint64_t G;
+    const uint32_t s = rowop::add_co(a.v, b.v, G);
+    const uint64_t P = __ballot(s == 0xffffffffu);
+    return {rowop::add_mask(s, carries_in(G, P))};
+}
+
 // lane-parallel CIOS Montgomery product.  Round i, lane j:  v = a_j b_i + t_j,
 // m = lo(v_0) (-p^-1), w = m p_j + lo(v_j), t_j <- hi(v_j) + hi(w_j) + lo(w_{j+1}).
 // The round's dependent chain is what a lone wave pays for (tools/latbench.hip), so m is taken
@@ -281,6 +301,10 @@ struct SqrCheaper<RFq> {
 template <>
 struct SqrCheaper<RFq2> {
     static constexpr bool value = false;
+};
+template <>
+struct ShiftOperands<RFq> {
+    static constexpr bool value = true;
 };
 
 // ---- memory: element `idx` of an array of 48-byte Fq; each row loads one element ------

@@ -14,6 +14,8 @@
 // processed 4 at a time.  Results equal jac_dbl / jac_add exactly (same formulas, same
 // branches); only the schedule differs.
 #pragma once
+#include <type_traits>
+
 #include "mbls_curve.hpp"
 #include "mbls_rowfield.hpp"
 
@@ -154,32 +156,55 @@ MBLS_DEV void sqr_mul(RFq2 (&rs)[KS], RFq2 (&rm)[KM], const RFq2 (&s)[KS], const
     }
 }
 
-// dbl-2009-l in 3 product levels (same result as jac_dbl)
+// dbl-2009-l in 3 product levels (same result as jac_dbl).
+// G1 rows (RFq): the constant factors ride on unreduced product operands (x2_in / x4_in /
+// x8_in: row shifts, add_in: no conditional subtraction), and the spare row of level 2 computes
+// 2D directly:
+//   L1: E = X (3X), B = Y^2, Z3 = (2Y) Z
+//   L2: F = E^2, D = (4X) B, 2D = (8X) B, 8C = (8B) B
+//   X3 = F - 2D;  L3: E (D - X3);  Y3 = E (D - X3) - 8C
+// -- 3 reduced subtractions on the chain instead of 12 additions / doublings / subtractions.
+// G2 rows (RFq2): an Fq2 square is 2 Fq products against 3 for a product, so the square
+// forms stay (levels of 7, 7 and 3 Fq products).
 template <class RF>
 MBLS_DEV Jacobian<RF> jdbl(const Jacobian<RF>& p) {
     if (p.is_inf()) return p;
-    // L1: A = X^2, B = Y^2 | YZ = Y*Z
-    RF s1[2], m1[1];
-    sqr_mul<2, 1>(s1, m1, {p.x, p.y}, {p.y}, {p.z});
-    const RF A = s1[0], B = s1[1];
-    const RF E = dbl(A) + A;
-    // L2: C = B^2, Fv = E^2 | XB = X*B  (D = 2((X + B)^2 - A - C) = 4 X B: a row product costs
-    // the same as a row square, and this form saves two additions)
-    RF s2[2], m2[1];
-    sqr_mul<2, 1>(s2, m2, {B, E}, {p.x}, {B});
-    const RF C = s2[0];
-    const RF D = dbl(dbl(m2[0]));
     Jacobian<RF> r;
-    r.x = s2[1] - dbl(D);
-    // L3: E * (D - X3)
-    RF m3[1];
-    mul<1>(m3, {E}, {D - r.x});
-    r.y = m3[0] - dbl(dbl(dbl(C)));
-    r.z = dbl(m1[0]);
+    if constexpr (std::is_same<RF, RFq>::value) {
+        RF m1[3];
+        mul<3>(m1, {p.x, p.y, x2_in(p.y)}, {add_in(x2_in(p.x), p.x), p.y, p.z});
+        const RF E = m1[0], B = m1[1];
+        RF m2[4];
+        mul<4>(m2, {E, x4_in(p.x), x8_in(p.x), x8_in(B)}, {E, B, B, B});
+        const RF D = m2[1];
+        r.x = m2[0] - m2[2];
+        RF m3[1];
+        mul<1>(m3, {E}, {D - r.x});
+        r.y = m3[0] - m2[3];
+        r.z = m1[2];
+    } else {
+        // L1: A = X^2, B = Y^2 | YZ = Y*Z
+        RF s1[2], m1[1];
+        sqr_mul<2, 1>(s1, m1, {p.x, p.y}, {p.y}, {p.z});
+        const RF A = s1[0], B = s1[1];
+        const RF E = dbl(A) + A;
+        // L2: C = B^2, Fv = E^2 | XB = X*B  (D = 4 X B)
+        RF s2[2], m2[1];
+        sqr_mul<2, 1>(s2, m2, {B, E}, {p.x}, {B});
+        const RF C = s2[0];
+        const RF D = dbl(dbl(m2[0]));
+        r.x = s2[1] - dbl(D);
+        // L3: E * (D - X3)
+        RF m3[1];
+        mul<1>(m3, {E}, {D - r.x});
+        r.y = m3[0] - dbl(dbl(dbl(C)));
+        r.z = dbl(m1[0]);
+    }
     return r;
 }
 
-// add-2007-bl in 5 product levels (same result and branches as jac_add)
+// add-2007-bl in 5 product levels (same result and branches as jac_add); for G1 rows 2H, 2R,
+// 2 Z1Z2 and 2 S1 are unreduced shifts feeding products (reduced doublings for Fq2)
 template <class RF>
 MBLS_DEV Jacobian<RF> jadd(const Jacobian<RF>& p, const Jacobian<RF>& q) {
     if (p.is_inf()) return q;
@@ -194,27 +219,28 @@ MBLS_DEV Jacobian<RF> jadd(const Jacobian<RF>& p, const Jacobian<RF>& q) {
     const RF U1 = m2[0], U2 = m2[1];
     const RF H = U2 - U1;
     // L3: S1 = Y1 Z2^3, S2 = Y2 Z1^3 | I = (2H)^2
+    const RF H2 = x2_in(H);
     RF s3[1], m3[2];
-    sqr_mul<1, 2>(s3, m3, {dbl(H)}, {p.y, q.y}, {m2[2], m2[3]});
+    sqr_mul<1, 2>(s3, m3, {H2}, {p.y, q.y}, {m2[2], m2[3]});
     const RF S1 = m3[0];
-    RF R = m3[1] - S1;
+    const RF R = m3[1] - S1;
     if (H.is_zero()) {
         if (R.is_zero()) return jdbl(p);
         return Jacobian<RF>::inf();
     }
     const RF I = s3[0];
-    R = dbl(R);
-    // L4: RR = R^2 | J = H I, V = U1 I, Z1Z2 H (Z3 = 2 Z1Z2 H)
+    const RF R2 = x2_in(R);
+    // L4: RR = (2R)^2 | J = H I, V = U1 I, Z3 = (2 Z1Z2) H
     RF s4[1], m4[3];
-    sqr_mul<1, 3>(s4, m4, {R}, {H, U1, m1[0]}, {I, I, H});
+    sqr_mul<1, 3>(s4, m4, {R2}, {H, U1, x2_in(m1[0])}, {I, I, H});
     const RF J = m4[0], V = m4[1];
     Jacobian<RF> r;
     r.x = s4[0] - J - dbl(V);
-    r.z = dbl(m4[2]);
-    // L5: R (V - X3), S1 J
+    r.z = m4[2];
+    // L5: 2R (V - X3), (2 S1) J
     RF m5[2];
-    mul<2>(m5, {R, S1}, {V - r.x, J});
-    r.y = m5[0] - dbl(m5[1]);
+    mul<2>(m5, {R2, x2_in(S1)}, {V - r.x, J});
+    r.y = m5[0] - m5[1];
     return r;
 }
 
