@@ -37,13 +37,17 @@ VEC_BYTES_PER_ELEM = 96    # read a, b; write out
 # v_mad_u64_u32 per G1 mixed addition (madd-2007-bl, lazy Y3): 5 Fq products x 288 + 4 squares x
 # 222 + one two-product lazy sum x 432
 MADS_PER_G1_MADD = 5 * 288 + 4 * 222 + 432
+# G2 (pair-sliced Fq2, psi split: 4 streams x 4 windows of 2^20 = 16.8 M mixed additions): one
+# Fq2 product = 2 lanes x one lazy Fq product-sum (432 mads), a square 2 x 288; madd-2007-bl in
+# Fq2 = 7 products + 4 squares
+MADS_PER_G2_MADD = 7 * 2 * 432 + 4 * 2 * 288
 # per Fr butterfly product (FIPS Fr: 64 product mads + 56 reduction mads, r = 1 mod 2^32)
 MADS_PER_FR_MUL = 120
 PROFILES = os.path.join(ROOT, "profiles")
 
 
 def pmc_summary():
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         path = os.path.join(PROFILES, rnd, "pmc_summary.json")
         try:
             with open(path) as f:
@@ -53,15 +57,21 @@ def pmc_summary():
     return {}, None
 
 
+def _pmc_kernel(kernel):
+    """per-launch counters of `kernel` (round-2 summaries keyed G1's accumulation "k_accumulate")"""
+    ks = pmc_summary()[0].get("kernels", {})
+    if kernel not in ks and kernel == "k_accumulate<G1>":
+        kernel = "k_accumulate"
+    return ks.get(kernel)
+
+
 def pmc_traffic(kernel):
-    d, _ = pmc_summary()
-    k = d.get("kernels", {}).get(kernel)
+    k = _pmc_kernel(kernel)
     return None if not k or k.get("hbm_bytes_per_launch") is None else k["hbm_bytes_per_launch"]
 
 
 def pmc_counter(kernel, counter):
-    d, _ = pmc_summary()
-    return d.get("kernels", {}).get(kernel, {}).get(counter)
+    return (_pmc_kernel(kernel) or {}).get(counter)
 
 
 # VALU issue cost in cycles per wave-instruction: v_mad_u64_u32 (an INT64 instruction) is
@@ -92,6 +102,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-budget-s", type=float, default=20.0, help="bound on the CPU MSM leg's repeats")
+    ap.add_argument("--no-cpu-total", action="store_true", help="skip the CPU config #4 MSM (2^msm_total_log, once)")
     ap.add_argument("--no-mix", action="store_true", help="skip the G2 MSM + batched NTT overlap leg (config #5)")
     ap.add_argument("--mix-batch", type=int, default=4, help="NTT polynomials in the config #5 batch")
     ap.add_argument("--msm-batch", type=int, default=8, help="members of the batched-MSM leg (0: skip)")
@@ -203,7 +214,7 @@ def main():
     if not args.headline_only:
         extra.update(msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_over_ranks, world))
     # ------------------------------------------------------------------ config #4: 2^total split over ranks
-    cfg4 = None
+    cfg4, cfg4_result = None, None
     if args.msm_total_log and not args.headline_only:
         total = 1 << args.msm_total_log
         lo, hi = sharded_msm.shard_range(total, world, rank)
@@ -222,6 +233,7 @@ def main():
                 "result_digest": digest(result),
                 "note": "same result_digest at every N = bit-identical sharded sum; the 1-GPU result is "
                         "pinned to the oracle by tests/test_gpu_parity.py::test_msm_g1_2_24_single_and_sharded"}
+        cfg4_result = result.clone()
         del s4, b4
         torch.cuda.empty_cache()
 
@@ -262,7 +274,7 @@ def main():
     # ------------------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.headline_only:
-        cpu = cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, x)
+        cpu = cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, x, cfg4_result)
 
     if rank == 0:
         def avg(prof, key):
@@ -279,7 +291,7 @@ def main():
         # mads issued: the committed INT64 counter (v_mad_u64_u32 plus a few 64-bit shifts and
         # compares) when present, else the algorithmic count (an upper estimate: a chunk's first
         # point costs no addition and its second the cheaper affine + affine step)
-        i64c = pmc_counter("k_accumulate", "SQ_INSTS_VALU_INT64")
+        i64c = pmc_counter("k_accumulate<G1>", "SQ_INSTS_VALU_INT64")
         mads_issued = i64c * 64 if i64c else contributions * MADS_PER_G1_MADD
         mad_t = mads_issued / (acc_ms * 1e-3) / 1e12 if acc_ms else None
         ntt_ach = NTT_BYTES_PER_ELEM * nn / (ntt_ms * 1e-3) / 1e9 if ntt_ms else None
@@ -313,7 +325,7 @@ def main():
                          "bound": "hbm", "achieved": round(msm_ach, 2) if msm_ach else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(msm_ach / HBM_PEAK_GBS, 5) if msm_ach else None,
-                         "traffic": pmc_traffic("k_accumulate"),
+                         "traffic": pmc_traffic("k_accumulate<G1>"),
                          "traffic_source": f"{pmc_src} (HBM bytes per launch)" if pmc_src else None,
                          "note": "VALU-bound (v_mad_u64_u32): see roofline_valu"},
             "roofline_valu": {"kernel": "k_accumulate<G1>", "bound": "valu",
@@ -322,10 +334,10 @@ def main():
                               "mads_per_launch": round(mads_issued),
                               "mads_source": "counter (SQ_INSTS_VALU_INT64 x 64)" if i64c else "algorithmic",
                               "mads_algorithmic_per_launch": contributions * MADS_PER_G1_MADD,
-                              "counter_int64_per_launch": (round(i64 * 64) if (i64 := pmc_counter("k_accumulate", "SQ_INSTS_VALU_INT64")) else None),
-                              "counter_valu_insts_per_launch": pmc_counter("k_accumulate", "SQ_INSTS_VALU"),
-                              "counter_issue_bound_ms": (round(b, 4) if (b := valu_issue_bound_ms("k_accumulate")) else None),
-                              "counter_issue_frac": (round(b / acc_ms, 4) if (b := valu_issue_bound_ms("k_accumulate")) and acc_ms else None),
+                              "counter_int64_per_launch": (round(i64 * 64) if (i64 := pmc_counter("k_accumulate<G1>", "SQ_INSTS_VALU_INT64")) else None),
+                              "counter_valu_insts_per_launch": pmc_counter("k_accumulate<G1>", "SQ_INSTS_VALU"),
+                              "counter_issue_bound_ms": (round(b, 4) if (b := valu_issue_bound_ms("k_accumulate<G1>")) else None),
+                              "counter_issue_frac": (round(b / acc_ms, 4) if (b := valu_issue_bound_ms("k_accumulate<G1>")) and acc_ms else None),
                               "counter_source": f"{pmc_src} (SQ_INSTS_VALU, SQ_INSTS_VALU_INT64 per launch)" if pmc_src else None,
                               "note": f"achieved = mads issued per launch / kernel time; algorithmic bound "
                                       f"{contributions} mixed additions x {MADS_PER_G1_MADD} mads; peak = measured "
@@ -372,6 +384,22 @@ def msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_ov
                                                  stream=stream, is_async=True, n=n), reps))
     out["msm_host_scalars_per_sec"] = round(world * 1e3 / hi_ms, 3)
     del host_s
+    # the reference's production call shape (core/msm.rs:594-682, msm_with_device_bases): PAGEABLE
+    # host Montgomery scalars (HostSlice over a Rust Vec), device bases, device result, then
+    # copy_to_host of the one point -- every byte through the boundary, timed per call
+    page_s = scalars.cpu().numpy().copy()  # ordinary (pageable) host memory
+    host_r = None
+
+    def pageable_call():
+        nonlocal host_r
+        amd.msm("g1", page_s, bases, icicle=True, scalars_mont=True, out=res, stream=stream, is_async=False, n=n)
+        host_r = res.cpu()
+    torch.cuda.synchronize(dev)
+    pg_ms = max_over_ranks(timed(pageable_call, reps))
+    out["msm_pageable_host_per_sec"] = round(world * 1e3 / pg_ms, 3)
+    out["msm_pageable_host_note"] = ("core/msm.rs:665-675 shape: pageable host scalars (32 MiB H2D), device bases, "
+                                     "device result copied to the host; PCIe-inclusive, never `value`")
+    del page_s
     # batched MSMs (ICICLE batch_size, shared device bases): members pipelined on two streams
     if args.msm_batch > 1:
         B = args.msm_batch
@@ -445,21 +473,64 @@ def mix_leg(args, amd, torch, dev, rank, timed):
 
     reps = max(2, min(args.steps, 5))
     g2_ms = timed(g2, reps)
+    res_iso = res.clone()
     ntt_ms = timed(ntts, reps)
+    yb_iso = yb.clone()
+    res.zero_()
+    yb.zero_()
+    torch.cuda.synchronize(dev)
     both_ms = timed(lambda: (g2(), ntts()), reps)
+    # the overlapped run must reproduce the isolated outputs bit for bit (the G2 result is pinned
+    # to the oracle by tests/test_gpu_parity.py::test_bench_msm_2_20_production_path[g2], the
+    # batch members by ::test_bench_ntt_2_22_single_and_batch4)
+    g2_same, ntt_same = bool(torch.equal(res, res_iso)), bool(torch.equal(yb, yb_iso))
+    assert g2_same and ntt_same, f"config #5 overlapped outputs differ from isolated: g2 {g2_same} ntt {ntt_same}"
+    del yb_iso
+    acc_ms = g2_stage_ms(amd, torch, dev, g2, s_a)
+    i64 = pmc_counter("k_accumulate<G2>", "SQ_INSTS_VALU_INT64")
+    contributions = 4 * n * ((64 + 16 - 1) // 16)  # psi split: 4n digit streams x 4 windows (c = 16)
+    mads = i64 * 64 if i64 else contributions * MADS_PER_G2_MADD
+    mad_t = mads / (acc_ms * 1e-3) / 1e12 if acc_ms else None
+    issue = valu_issue_bound_ms("k_accumulate<G2>")
     return {"g2_msm_points": n, "ntt_batch": B, "ntt_size": nn, "g2_msm_ms": round(g2_ms, 3),
             "g2_msm_per_sec": round(1e3 / g2_ms, 3),
             "g2_roofline_hbm_frac": round(G2_BYTES_PER_POINT * n / (g2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "g2_accumulate_ms": round(acc_ms, 4) if acc_ms else None,
+            "g2_roofline_valu": {"kernel": "k_accumulate<G2> (pair-sliced Fq2 lanes)", "bound": "valu",
+                                 "achieved": round(mad_t, 3) if mad_t else None, "peak": MAD_RATE_T,
+                                 "unit": "T v_mad_u64_u32/s",
+                                 "frac": round(mad_t / MAD_RATE_T, 4) if mad_t else None,
+                                 "mads_per_launch": round(mads),
+                                 "mads_source": "counter (SQ_INSTS_VALU_INT64 x 64)" if i64 else "algorithmic",
+                                 "counter_issue_bound_ms": round(issue, 4) if issue else None,
+                                 "counter_issue_frac": round(issue / acc_ms, 4) if issue and acc_ms else None},
             "batched_ntt_ms": round(ntt_ms, 3), "overlapped_ms": round(both_ms, 3),
             "sum_isolated_ms": round(g2_ms + ntt_ms, 3), "streams": 2,
+            "overlap_note": "both legs are VALU-bound (Montgomery products on v_mad_u64_u32), so two streams "
+                            "mostly time-slice the SIMDs: the overlap only hides launch gaps and the G2 MSM's "
+                            "latency-bound tail, a few percent",
+            "overlapped_outputs_bit_identical": g2_same and ntt_same,
             "g2_result_digest": digest(res)}
 
 
-def cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, ntt_in):
+def g2_stage_ms(amd, torch, dev, g2, st):
+    """average k_accumulate<G2> stage time (HIP events on the MSM's stream)"""
+    amd.profile(True)
+    for _ in range(3):
+        g2()
+    st.synchronize()
+    prof = amd.profile_read()
+    amd.profile(False)
+    ms, cnt = prof.get("msm.accumulate", (0.0, 0))
+    return ms / cnt if cnt else None
+
+
+def cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, ntt_in, cfg4_result=None):
     """The oracle (oracle/bls12_381_oracle.c: C restatement of the reference CPU semantics,
     OpenMP Pippenger / radix-2 NTT / vecops) on the host cores, on the SAME inputs as the GPU
-    legs.  MSM: median of repeated full 2^msm_log runs within --cpu-budget-s, and the result
-    must equal the GPU headline result (bit_exact).  BLST is not available."""
+    legs.  Protocol: one untimed warmup, then the median of >= 5 runs for the
+    2^msm_log G1 MSM (bounded by --cpu-budget-s), the NTTs and the G2 MSM; config #4's 2^24 G1 MSM
+    once.  Each MSM result must equal the GPU's (bit_exact).  BLST is not available."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import gpu_helpers
@@ -473,29 +544,30 @@ def cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, ntt_in):
     one = np.zeros((n, 4), dtype=np.uint64)
     one[:, 0] = 1
     o.orc_vec_mul(H.ptr(s_std), H.ptr(s_mont), H.ptr(one), n)
-    times, ref = [], None
-    t_start = time.perf_counter()
-    while len(times) < 5 and (len(times) < 2 or time.perf_counter() - t_start < args.cpu_budget_s):
-        t0 = time.perf_counter()
-        ref = H.oracle_msm("g1", s_std, b, threads=threads)
-        times.append(time.perf_counter() - t0)
-    msm_s = statistics.median(times)
+
+    def med(fn, runs=5, budget_s=None):
+        fn()  # warmup
+        ts, t_start = [], time.perf_counter()
+        while len(ts) < runs and (budget_s is None or len(ts) < 2 or time.perf_counter() - t_start < budget_s):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts), len(ts)
+
+    ref = H.oracle_msm("g1", s_std, b, threads=threads)
+    msm_s, runs = med(lambda: H.oracle_msm("g1", s_std, b, threads=threads), 5, args.cpu_budget_s)
     got = gpu_helpers.decode_icicle("g1", amd.to_numpy_u64(headline_result)[0])
     bit_exact = got == H.g1_from_affine_mont(ref)
     out = {"value": round(1.0 / msm_s, 4), "unit": "MSM/s", "cores": threads, "kind": "port",
-           "sample": f"full G1 MSM of 2^{args.msm_log} points on the headline's inputs, median of {len(times)} "
-                     f"runs, oracle/bls12_381_oracle.c OpenMP Pippenger on {threads} threads; BLST not available",
+           "sample": f"full G1 MSM of 2^{args.msm_log} points on the headline's inputs, median of {runs} runs after "
+                     f"one warmup, oracle/bls12_381_oracle.c OpenMP Pippenger on {threads} threads; BLST not available",
            "bit_exact": bool(bit_exact)}
     # NTT (config #2 / the metric's second half): oracle radix-2 best_fft, all threads
     xn = np.ascontiguousarray(amd.to_numpy_u64(ntt_in))
     for log_n in (20, args.ntt_log):
         a = np.ascontiguousarray(xn[: 1 << log_n])
-        ts = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            H.oracle_ntt(a, log_n, False, threads=threads)
-            ts.append(time.perf_counter() - t0)
-        out[f"ntt_2^{log_n}_ms"] = round(statistics.median(ts) * 1e3, 2)
+        t, _ = med(lambda: H.oracle_ntt(a, log_n, False, threads=threads), 5)
+        out[f"ntt_2^{log_n}_ms"] = round(t * 1e3, 2)
     # vecops 2^16 (config #1: the CPU path of MIDNIGHT_DEVICE=cpu, core/vecops.rs:575-610)
     va = np.ascontiguousarray(xn[: 1 << 16])
     vb = np.ascontiguousarray(xn[1 << 16: 2 << 16])
@@ -503,24 +575,44 @@ def cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, ntt_in):
     for th, tag in ((1, "1t"), (threads, f"{threads}t")):
         o.orc_set_threads(th)
         for op, fn in (("add", o.orc_vec_add), ("mul", o.orc_vec_mul)):
-            ts = []
-            for _ in range(20):
-                t0 = time.perf_counter()
-                fn(H.ptr(vc), H.ptr(va), H.ptr(vb), 1 << 16)
-                ts.append(time.perf_counter() - t0)
-            out[f"vec_{op}_2^16_{tag}_us"] = round(statistics.median(ts) * 1e6, 1)
+            t, _ = med(lambda: fn(H.ptr(vc), H.ptr(va), H.ptr(vb), 1 << 16), 20)
+            out[f"vec_{op}_2^16_{tag}_us"] = round(t * 1e6, 1)
     o.orc_set_threads(0)
-    # G2 MSM (config #5): one full 2^msm_log run on the mix leg's inputs
+    out["protocol"] = "median of >= 5 runs after one untimed warmup (MSM 2^20, NTT, G2); 20 runs for vecops"
+    # G2 MSM (config #5) on the mix leg's inputs
     if not args.no_mix:
         g2s = torch.zeros((n, 4), dtype=torch.int64, device=scalars.device)
         g2b = torch.zeros((n, 24), dtype=torch.int64, device=scalars.device)
         amd.gen_scalars(g2s, 0x5EED0005, montgomery=False)
         amd.gen_bases("g2", g2b, 0x5EED0015)
         torch.cuda.synchronize()
+        g2sn = np.ascontiguousarray(amd.to_numpy_u64(g2s))
+        g2bn = np.ascontiguousarray(amd.to_numpy_u64(g2b))
+        del g2s, g2b
+        t, runs = med(lambda: H.oracle_msm("g2", g2sn, g2bn, threads=threads), 5)
+        out[f"g2_msm_2^{args.msm_log}_ms"] = round(t * 1e3, 1)
+        out["g2_msm_runs"] = runs
+        del g2sn, g2bn
+    # config #4: the 2^msm_total_log G1 MSM once, bit-exact against the GPU's (1-GPU) result
+    if args.msm_total_log and not args.no_cpu_total and cfg4_result is not None:
+        total = 1 << args.msm_total_log
+        s4 = torch.zeros((total, 4), dtype=torch.int64, device=scalars.device)
+        amd.gen_scalars(s4, 0x5EED0004, montgomery=False)
+        s4n = np.ascontiguousarray(amd.to_numpy_u64(s4))
+        del s4
+        b4 = torch.zeros((total, 12), dtype=torch.int64, device=scalars.device)
+        amd.gen_bases("g1", b4, 0x5EED0013)
+        b4n = np.ascontiguousarray(amd.to_numpy_u64(b4))
+        del b4
+        torch.cuda.empty_cache()
         t0 = time.perf_counter()
-        H.oracle_msm("g2", np.ascontiguousarray(amd.to_numpy_u64(g2s)), np.ascontiguousarray(amd.to_numpy_u64(g2b)),
-                     threads=threads)
-        out[f"g2_msm_2^{args.msm_log}_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        r4 = H.oracle_msm("g1", s4n, b4n, threads=threads)
+        t4 = time.perf_counter() - t0
+        got4 = gpu_helpers.decode_icicle("g1", amd.to_numpy_u64(cfg4_result)[0])
+        out[f"g1_msm_2^{args.msm_total_log}_ms"] = round(t4 * 1e3, 1)
+        out[f"g1_msm_2^{args.msm_total_log}_note"] = "config #4 on the CPU: timed once (SURVEY.md 8d row #4)"
+        out[f"g1_msm_2^{args.msm_total_log}_bit_exact"] = bool(got4 == H.g1_from_affine_mont(r4))
+        del s4n, b4n
     return out
 
 

@@ -151,6 +151,9 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
 #ifndef MBLS_ACC_MMADD
 #define MBLS_ACC_MMADD 1
 #endif
+#ifndef MBLS_ACC_LDS
+#define MBLS_ACC_LDS 1  // G1: next point prefetched into LDS (LDS-DMA) instead of VGPRs
+#endif
 template <class F, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets,
                                                     const uint32_t* __restrict__ chunk_off,
@@ -178,10 +181,10 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
         idx = idx >= nsplit ? idx - nsplit : idx;
         return load_affine<L>(src, idx);
     };
-    // one point ahead: the next random 96/192-byte fetch overlaps this mixed addition
-    uint32_t v = sorted[beg];
-    Affine<L> p = fetch(v);
-    for (uint32_t e = beg; e < end; ++e) {
+    // second point of the chunk (the same step for every lane of the wave): the accumulator is
+    // still the first point, Z = 1, so the affine + affine formula applies (~55% of a mixed
+    // addition); a bucket boundary at this step left it at the identity instead
+    auto step = [&](uint32_t e, const Affine<L>& q) {
         if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
             store_jac<L>(partials, seg, acc);
             acc = Jacobian<L>::inf();
@@ -191,17 +194,58 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
             seg = chunk_off[b];
             bend = offsets[b + 1];
         }
-        const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
-        const Affine<L> pn = fetch(vn);
-        const Affine<L> q = (v & 1) ? aff_neg(p) : p;
-        // second point of the chunk (the same step for every lane of the wave): the accumulator
-        // is still the first point, Z = 1, so the affine + affine formula applies (~55% of a
-        // mixed addition); a bucket boundary at this step left it at the identity instead
         bool done = false;
         if (MBLS_ACC_MMADD && e == beg + 1 && !acc.is_inf() && !q.is_inf()) done = jac_mmadd(acc, q, acc);
         if (!done) acc = jac_madd(acc, q);
-        v = vn;
-        p = pn;
+    };
+    uint32_t v = sorted[beg];
+    if constexpr (std::is_same<L, Fq>::value && MBLS_ACC_LDS) {
+        // G1: the next point is prefetched into LDS by LDS-DMA (global_load_lds_dwordx4: six
+        // 16-byte pieces per lane, no VGPR destination), double-buffered per wave, instead of
+        // into 24 VGPRs held across the mixed addition: the accumulation fits its 168-VGPR /
+        // 3-waves-per-SIMD bound without spills.  Stage: [slot][wave][piece][lane] x 16 B.
+        __shared__ uint4 stage[2][256 / 64][6][64];
+        const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        auto issue = [&](uint32_t vv, uint32_t slot) {
+            uint32_t idx = vv >> 1;
+            const uint8_t* src = idx >= nsplit ? phi : bases;
+            idx = idx >= nsplit ? idx - nsplit : idx;
+            const uint8_t* g = src + (size_t)idx * 96;
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(g + 16 * k),
+                                                 (__attribute__((address_space(3))) void*)&stage[slot][wv][k][0], 16, 0, 0);
+        };
+        issue(v, 0);
+        uint32_t vn = beg + 1 < end ? sorted[beg + 1] : v;
+        uint32_t it = 0;
+        for (uint32_t e = beg; e < end; ++e, ++it) {
+            const uint32_t slot = it & 1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this point's pieces have landed
+            Affine<Fq> p;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint4 xa = stage[slot][wv][k][ln], ya = stage[slot][wv][3 + k][ln];
+                p.x.v[4 * k] = xa.x, p.x.v[4 * k + 1] = xa.y, p.x.v[4 * k + 2] = xa.z, p.x.v[4 * k + 3] = xa.w;
+                p.y.v[4 * k] = ya.x, p.y.v[4 * k + 1] = ya.y, p.y.v[4 * k + 2] = ya.z, p.y.v[4 * k + 3] = ya.w;
+            }
+            // the other slot was read one full addition ago: safe to overwrite
+            if (e + 1 < end) issue(vn, slot ^ 1u);
+            const uint32_t vnn = e + 2 < end ? sorted[e + 2] : vn;
+            step(e, (v & 1) ? aff_neg(p) : p);
+            v = vn;
+            vn = vnn;
+        }
+    } else {
+        // one point ahead: the next random 96/192-byte fetch overlaps this mixed addition
+        Affine<L> p = fetch(v);
+        for (uint32_t e = beg; e < end; ++e) {
+            const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
+            const Affine<L> pn = fetch(vn);
+            step(e, (v & 1) ? aff_neg(p) : p);
+            v = vn;
+            p = pn;
+        }
     }
     store_jac<L>(partials, seg, acc);
 }
@@ -932,7 +976,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         ProfScope ps("msm.bucket_sum", st);
         // heavy buckets (> SMALL_MAX chunks; no-op passes for random inputs) on the side stream,
         // concurrently with the light ones: disjoint partials / buckets
-        if (max_per_bucket > SMALL_MAX) {
+        static const bool skip_heavy = getenv("MBLS_DIAG_SKIP_HEAVY") != nullptr;  // TEMP timing probe
+        if (max_per_bucket > SMALL_MAX && !skip_heavy) {
             MBLS_TRY(hipEventRecord(ev[2], st));
             MBLS_TRY(hipStreamWaitEvent(side, ev[2], 0));
             for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
@@ -944,7 +989,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         }
         hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB * LN + 255) / 256), dim3(256), 0, st, chunk_off, perm, binbase,
                            0u, order_words(TB), partials, buckets);
-        if (max_per_bucket > SMALL_MAX) MBLS_TRY(hipStreamWaitEvent(st, ev[3], 0));
+        if (max_per_bucket > SMALL_MAX && !skip_heavy) MBLS_TRY(hipStreamWaitEvent(st, ev[3], 0));
     }
     ProfScope ps_red("msm.reduce", st);
     // recursive running-sum reduction.  The per-level T tree sums are latency-bound chains off

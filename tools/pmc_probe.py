@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Fixed workload for PMC passes (tools/gpu_pmc.sh): `--reps` G1 MSMs of 2^20 (bench.py's
 headline inputs and call: ICICLE entry, Montgomery scalars, device bases and result) and
-`--reps` forward Fr NTTs of 2^22, nothing else, so per-kernel counter averages are per launch
+`--reps` forward Fr NTTs of 2^22, `--g2-reps` G2 MSMs of 2^20 (config #5 inputs), nothing else, so per-kernel counter averages are per launch
 of exactly the benchmarked configurations."""
 import argparse
 import os
@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--msm-log", type=int, default=20)
     ap.add_argument("--ntt-log", type=int, default=22)
+    ap.add_argument("--g2-reps", type=int, default=2, help="G2 MSMs of 2^msm_log (config #5 inputs)")
     a = ap.parse_args()
     import torch
     import bls12_381_amd as amd
@@ -29,6 +30,16 @@ def main():
     for _ in range(a.reps):
         amd.msm("g1", s, b, icicle=True, scalars_mont=True, out=out, is_async=True, n=n)
     torch.cuda.synchronize()
+    if a.g2_reps:
+        s2 = torch.zeros((n, 4), dtype=torch.int64, device=dev)
+        b2 = torch.zeros((n, 24), dtype=torch.int64, device=dev)
+        amd.gen_scalars(s2, 0x5EED0005, montgomery=True)
+        amd.gen_bases("g2", b2, 0x5EED0015)
+        o2 = torch.zeros((1, 36), dtype=torch.int64, device=dev)
+        for _ in range(a.g2_reps):
+            amd.msm("g2", s2, b2, icicle=True, scalars_mont=True, out=o2, is_async=True, n=n)
+        torch.cuda.synchronize()
+        del s2, b2
     amd.ntt_init_domain()
     x = torch.zeros((1 << a.ntt_log, 4), dtype=torch.int64, device=dev)
     y = torch.zeros_like(x)
