@@ -28,12 +28,15 @@ MBLS_DEV uint32_t row() { return (__lane_id() >> 4) & 3u; }
 template <int K>
 MBLS_DEV void mul4(RFq* r, const RFq* a, const RFq* b) {
     static_assert(K >= 1 && K <= 4, "one product per row");
-    const uint32_t w = row();
+    // row k takes operand k: v_cndmask with the constant lane mask of row k (inline asm -- a
+    // select chain on row() was turned into a dynamically indexed stack array, i.e. a scratch
+    // store + load on every product level of the latency-bound chains)
     uint32_t A = a[0].v, B = b[0].v;
 #pragma unroll
     for (int k = 1; k < K; ++k) {
-        A = (w == (uint32_t)k) ? a[k].v : A;
-        B = (w == (uint32_t)k) ? b[k].v : B;
+        const uint64_t rowk = 0xffffull << (16 * k);
+        A = rowop::pick(rowk, A, a[k].v);
+        B = rowop::pick(rowk, B, b[k].v);
     }
     const RFq p = RFq{A} * RFq{B};
     const int l16 = (int)rowdpp::lane16();

@@ -539,6 +539,10 @@ static constexpr int DT_THREADS = 1024;
 #endif
 static constexpr int DT_PER = MBLS_DT_PER;  // indices per thread
 static constexpr uint32_t DT_TILE = DT_THREADS * DT_PER;
+// gfx950 workgroup LDS limit (160 KiB per workgroup, the whole CU; MI355X_MICROARCH.md): the
+// digit pass stages a whole tile (DT_TILE words) beside its 256-word part histogram
+static constexpr size_t LDS_LIMIT_BYTES = 160 * 1024;
+static_assert(DT_TILE * 4 + (256 + 1) * 4 <= LDS_LIMIT_BYTES, "MBLS_DT_PER too large: k_digits_part's LDS stage overflows");
 static constexpr uint32_t DT_MAX_B = 1u << 15;
 
 template <bool MONT>
@@ -998,6 +1002,7 @@ static constexpr uint32_t PS_TEAM = MBLS_PS_TEAM;
 #define MBLS_PS_STAGE 9216
 #endif
 static constexpr uint32_t PS_STAGE = MBLS_PS_STAGE;
+static_assert(PS_STAGE * 4 + (2 * 128 + 1) * 4 <= LDS_LIMIT_BYTES, "MBLS_PS_STAGE too large for the workgroup LDS");
 
 template <bool PACK>
 __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ ent, const uint32_t* __restrict__ seg_off,
@@ -1095,8 +1100,8 @@ eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, c
     ZeroList zl;
     zl.p[0] = part_tot;  // k_digits_part's per-part totals (atomics)
     zl.n[0] = (uint32_t)P.Wg * z.NP;
-    zl.p[1] = zero_word;  // the chunk-count maximum (k_chunk_counts' atomicMax)
-    zl.n[1] = zero_word ? 1u : 0u;
+    zl.p[1] = zero_word;  // the chunk-count maximum (k_chunk_counts' atomicMax), HeavyTab counters
+    zl.n[1] = zero_word ? 3u : 0u;
     eIcicleError er = digit_sources(scalars, mont, n, P, dsrc, zl, st, src, nidx);
     if (er != MBLS_SUCCESS) return er;
     dim3 g(z.segments), b(DT_THREADS);
@@ -1202,7 +1207,7 @@ __global__ __launch_bounds__(256) void k_chunk_counts(const uint32_t* counts, co
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
                                  uint32_t L, uint32_t* binhist, uint32_t groups, bool zeroed, uint32_t* cloc,
                                  uint32_t* blk_tot, hipStream_t st) {
-    if (!zeroed) MBLS_TRY(hipMemsetAsync(nchunks + m, 0, 4, st));
+    if (!zeroed) MBLS_TRY(hipMemsetAsync(nchunks + m, 0, 12, st));  // maximum + HeavyTab counters
     const uint32_t nblk = (m + 255) / 256;
     hipLaunchKernelGGL(k_chunk_counts, dim3(nblk), dim3(256), 0, st, counts, offsets, nchunks, m, L, binhist,
                        nblk / groups, cloc, blk_tot);
@@ -1284,10 +1289,10 @@ __global__ __launch_bounds__(256) void k_chunk_owner(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ offsets,
                                                      uint32_t m, uint32_t L, uint32_t* __restrict__ owner,
                                                      uint32_t* __restrict__ first, const uint32_t* __restrict__ nchunks,
-                                                     const uint32_t* __restrict__ binbase, uint32_t bpg,
-                                                     uint32_t* __restrict__ perm) {
+                                                     const uint32_t* __restrict__ binbase, uint32_t* __restrict__ perm,
+                                                     HeavyTab H) {
     __shared__ uint32_t cur[ORDER_BINS];
-    if (threadIdx.x < ORDER_BINS) cur[threadIdx.x] = binbase[order_index(blockIdx.x, threadIdx.x, bpg)];
+    if (threadIdx.x < ORDER_BINS) cur[threadIdx.x] = binbase[order_index(blockIdx.x, threadIdx.x, gridDim.x)];
     __syncthreads();
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
@@ -1299,16 +1304,27 @@ __global__ __launch_bounds__(256) void k_chunk_owner(const uint32_t* __restrict_
     const uint32_t o = offsets[b], e = offsets[b + 1];
     for (uint32_t t = (o + L - 1) / L; t * L < e; ++t) first[t] = b;
     const uint32_t c = nchunks[b];
-    if (c <= SMALL_MAX) perm[atomicAdd(&cur[c], 1u)] = b;
+    if (c <= SMALL_MAX) {
+        perm[atomicAdd(&cur[c], 1u)] = b;
+    } else {  // heavy bucket (adversarial inputs only): list it with its slices for k_bucket_small
+        const uint32_t ns = (c + HEAVY_SLICE - 1) / HEAVY_SLICE;
+        const uint32_t ent = atomicAdd(&H.cnt[0], 1u);
+        const uint32_t f0 = atomicAdd(&H.cnt[1], ns);
+        H.bucket[ent] = b;
+        H.first[ent] = f0;
+        H.nslices[ent] = ns;
+        H.done[ent] = 0;
+        for (uint32_t k = 0; k < ns; ++k) H.owner[f0 + k] = ent;
+    }
 }
 
 eIcicleError launch_chunk_owner(const uint32_t* cloc, const uint32_t* blk_pre, uint32_t* chunk_off,
                                 const uint32_t* offsets, uint32_t m, uint32_t L, uint32_t* owner, uint32_t* first,
-                                const uint32_t* nchunks, const uint32_t* binbase, uint32_t groups, uint32_t* perm,
+                                const uint32_t* nchunks, const uint32_t* binbase, uint32_t* perm, HeavyTab H,
                                 hipStream_t st) {
     const uint32_t nblk = (m + 255) / 256;
     hipLaunchKernelGGL(k_chunk_owner, dim3(nblk), dim3(256), 0, st, cloc, blk_pre, chunk_off, offsets, m, L, owner,
-                       first, nchunks, binbase, nblk / groups, perm);
+                       first, nchunks, binbase, perm, H);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }

@@ -16,13 +16,12 @@
 //                     (k_digits_part + k_part_sort, msm_common.hip 2b).
 //   4. k_accumulate   one thread per chunk: sum of +-P_i by mixed additions -> partial.
 //   5. k_bucket_sum   one thread per bucket: sum of its chunk partials.
-//   6. bucket reduction sum_d d*B_d per window as a recursive running-sum: level l splits
-//                     its M inputs in segments of SEG, producing T_q = sum_t (t+off) V_t and
-//                     R_q = sum_t V_t; R becomes the next level's input (weight q), and
-//                     G_w = sum T0 + SEG*(sum T1 + SEG*(...)).  No scalar multiplications,
-//                     every thread chain is 2*SEG additions.
-//   7. k_tree_sum     per-window LDS tree sums of each level's T; k_window_horner folds the
-//                     levels; k_final folds the windows: sum_w 2^(c w) G_w.
+//   6. bucket reduction sum_d d*B_d per window as a recursive running sum (k_reduce_scaled):
+//                     level l splits its inputs in segments of 2^s; each segment's chain walks
+//                     R += V_t, S += R, S += U_t and outputs U' = S and V' = 2^s R, so every level's
+//                     outputs carry weight 1 and the last level's output IS the window sum (no
+//                     scalar multiplications, no per-level tree sums, no window Horner).
+//   7. k_final*       fold over windows: sum_w 2^(c w) G_w (+ ICICLE normalisation).
 // Precompute factor F (bases table = F blocks of n bases, block f = 2^(c*Wg*f) * P) folds
 // the W windows into Wg = ceil(W/F) groups so the final fold shrinks to (Wg-1)*c doublings.
 #pragma once
@@ -88,11 +87,6 @@ struct MsmPlan {
     uint8_t seg_log[MAX_LEVELS];   // log2 segment length per level
     uint8_t mode[MAX_LEVELS];      // MODE_LANE / MODE_ROW / MODE_WAVE per level
     uint32_t seg(int l) const { return 1u << seg_log[l]; }
-    uint64_t seg_logs_packed() const {  // 4 bits per level, for k_window_horner
-        uint64_t v = 0;
-        for (int l = 0; l < levels; ++l) v |= (uint64_t)seg_log[l] << (4 * l);
-        return v;
-    }
 };
 
 // endo: the split the group offers (1 none, 2 G1 GLV, 4 G2 psi); make_plan decides whether to use it
@@ -114,9 +108,21 @@ eIcicleError launch_order_scan(const uint32_t* binhist, uint32_t* binbase, uint3
 uint32_t order_words(uint32_t m);
 eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const uint32_t* ranks, size_t total,
                             const uint32_t* offsets, uint32_t* sorted, hipStream_t st);
+// heavy buckets (> SMALL_MAX chunk partials), listed by k_chunk_owner for k_bucket_small's slice
+// workgroups.  cnt[0] = heavy buckets, cnt[1] = slices: words TB + 1, TB + 2 of the chunk-count
+// array, zeroed by the digit pass with the chunk-count maximum at TB.
+struct HeavyTab {
+    uint32_t* cnt;
+    uint32_t* bucket;   // entry e -> its bucket
+    uint32_t* first;    // entry e -> its first slice
+    uint32_t* nslices;  // entry e -> its slice count
+    uint32_t* done;     // entry e -> slices finished (last-block-done counter)
+    uint32_t* owner;    // slice g -> its entry
+    uint8_t* res;       // slice g -> its sum (Jacobian)
+};
 eIcicleError launch_chunk_owner(const uint32_t* cloc, const uint32_t* blk_pre, uint32_t* chunk_off,
                                 const uint32_t* offsets, uint32_t m, uint32_t L, uint32_t* owner, uint32_t* first,
-                                const uint32_t* nchunks, const uint32_t* binbase, uint32_t groups, uint32_t* perm,
+                                const uint32_t* nchunks, const uint32_t* binbase, uint32_t* perm, HeavyTab H,
                                 hipStream_t st);
 eIcicleError launch_scalars_from_mont(uint8_t* s, size_t n, hipStream_t st);
 eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
@@ -251,62 +257,85 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
 }
 
 // ------------------------------------------------------------------------------------
-// 5. bucket sums from chunk partials: in-place tree over the chunks of each bucket with
-//    fan-in TREE_FANIN per pass, so a bucket holding many chunks (adversarial inputs) costs
-//    log passes instead of one serial thread.  Passes past the largest bucket exit at once
-//    (maxc = max chunks per bucket, computed on device).
+// 5. bucket sums from chunk partials.  Light buckets (<= SMALL_MAX partials -- every bucket of
+//    random inputs): one thread each.  Heavy buckets (equal scalars, adversarial inputs): cut into
+//    slices of HEAVY_SLICE partials, listed by k_chunk_owner (HeavyTab); one workgroup per slice
+//    sums its slice (strided chains + an LDS tree), and the workgroup that finishes a bucket's
+//    last slice (a counter per bucket: last-block-done) sums the bucket's slice sums.  The slice
+//    workgroups ride in the same launch as the light buckets (HEAVY_BLOCKS extra workgroups that
+//    exit at once when there is no heavy bucket): no extra launch, no side stream, no event.
 // ------------------------------------------------------------------------------------
-static constexpr int TREE_FANIN = 8;
-// grid cap of the heavy-bucket passes (grid-stride): for random inputs every pass exits at once,
-// and its workgroups only compete with k_bucket_small for dispatch
-#ifndef MBLS_HEAVY_GRID
-#define MBLS_HEAVY_GRID 1024u
-#endif
+static constexpr uint32_t HEAVY_SLICE = 2048;  // chunk partials per heavy slice (one workgroup)
+static constexpr uint32_t HEAVY_BLOCKS = 256;  // workgroups appended to k_bucket_small
+
+// one workgroup's chains hold partial sums: LDS tree, the total ends in chain 0
+template <class L>
+MBLS_DEV Jacobian<L> block_tree(Jacobian<L> acc, uint8_t* sh, uint32_t j, uint32_t chains) {
+    store_jac<L>(sh, j, acc);
+    __syncthreads();
+    for (uint32_t s = chains / 2; s > 0; s >>= 1) {
+        if (j < s) {
+            acc = jac_add(acc, load_jac<L>(sh, j + s));
+            store_jac<L>(sh, j, acc);
+        }
+        __syncthreads();
+    }
+    return acc;
+}
 
 template <class F>
-__global__ __launch_bounds__(256) void k_bucket_tree(const uint32_t* __restrict__ chunk_off,
-                                                     const uint32_t* __restrict__ owner, uint32_t b0, uint32_t b1,
-                                                     uint32_t max_chunks, const uint32_t* __restrict__ maxc,
-                                                     uint32_t step, uint8_t* __restrict__ partials) {
-    MBLS_TAIL_PRIO();
+MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ partials,
+                           uint8_t* __restrict__ buckets, const HeavyTab& H, uint32_t hb, uint32_t nhb) {
     using L = typename LaneOf<F>::type;
     constexpr uint32_t LN = LaneOf<F>::LANES;
-    if (*maxc <= SMALL_MAX || step >= *maxc) return;  // only heavy buckets remain
-    const uint32_t total = min(max_chunks, chunk_off[b1]);
-    // capped grid, grid-stride: a pass that finds no work costs one small launch
-    for (uint32_t ch = chunk_off[b0] + (blockIdx.x * blockDim.x + threadIdx.x) / LN; ch < total;
-         ch += gridDim.x * blockDim.x / LN) {
-        const uint32_t b = owner[ch];
-        const uint32_t j = ch - chunk_off[b];
-        const uint32_t cnt = chunk_off[b + 1] - chunk_off[b];
-        if (cnt <= SMALL_MAX) continue;  // summed by k_bucket_small
-        if (j % (TREE_FANIN * step) != 0 || j + step >= cnt) continue;
-        Jacobian<L> acc = load_jac<L>(partials, ch);
-        for (int g = 1; g < TREE_FANIN; ++g) {
-            uint32_t o = j + g * step;
-            if (o >= cnt) break;
-            acc = jac_add(acc, load_jac<L>(partials, (size_t)ch + g * step));
+    constexpr uint32_t CHAINS = 256 / LN;
+    __shared__ __attribute__((aligned(16))) uint8_t sh[CHAINS * 3 * sizeof(F)];
+    __shared__ uint32_t last;
+    const uint32_t nsl = H.cnt[1];
+    const uint32_t j = threadIdx.x / LN;
+    for (uint32_t g = hb; g < nsl; g += nhb) {
+        const uint32_t e = H.owner[g], b = H.bucket[e];
+        const uint32_t c0 = chunk_off[b] + (g - H.first[e]) * HEAVY_SLICE;
+        const uint32_t c1 = min(c0 + HEAVY_SLICE, chunk_off[b + 1]);
+        Jacobian<L> acc = Jacobian<L>::inf();
+        for (uint32_t k = c0 + j; k < c1; k += CHAINS) acc = jac_add(acc, load_jac<L>(partials, k));
+        acc = block_tree<L>(acc, sh, j, CHAINS);
+        if (j == 0) store_jac<L>(H.res, g, acc);
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) last = atomicAdd(&H.done[e], 1u) + 1 == H.nslices[e] ? 1u : 0u;
+        __syncthreads();
+        if (last) {  // this workgroup finished bucket b's last slice: sum the slice sums
+            __threadfence();
+            const uint32_t ns = H.nslices[e], f0 = H.first[e];
+            Jacobian<L> tot = Jacobian<L>::inf();
+            for (uint32_t k = j; k < ns; k += CHAINS) tot = jac_add(tot, load_jac<L>(H.res, f0 + k));
+            tot = block_tree<L>(tot, sh, j, CHAINS);
+            if (j == 0) store_jac<L>(buckets, b, tot);
         }
-        store_jac<L>(partials, ch, acc);
+        __syncthreads();  // sh and `last` are reused by the next slice
     }
 }
 
-// common case: one thread per light bucket (<= SMALL_MAX chunks) sums its chunk partials;
-// thread t of window group g takes perm[start_g + t] (k_bucket_order: buckets grouped by group,
-// then by chunk count, so a wave's lanes run the same number of additions).  The group's range
-// of perm comes from the order scan: binbase at the group's first histogram word, and the next
-// group's (the scan total for the last group).
+// light buckets: one thread per bucket (<= SMALL_MAX chunks) sums its chunk partials; thread t
+// takes perm[start + t] (k_chunk_owner: buckets grouped by chunk count, heaviest first, so a
+// wave's lanes run the same number of additions).  Workgroups from `light_blocks` on take the
+// heavy slices.
 template <class F>
 #ifndef MBLS_BS_MINW
 #define MBLS_BS_MINW 1
 #endif
 __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32_t* __restrict__ chunk_off,
                                                       const uint32_t* __restrict__ perm, const uint32_t* __restrict__ binbase,
-                                                      uint32_t g, uint32_t gwords, const uint8_t* __restrict__ partials,
-                                                      uint8_t* __restrict__ buckets) {
+                                                      uint32_t gwords, const uint8_t* __restrict__ partials,
+                                                      uint8_t* __restrict__ buckets, uint32_t light_blocks, HeavyTab H) {
     MBLS_TAIL_PRIO();
     using L = typename LaneOf<F>::type;
-    const uint32_t start = binbase[g * gwords], stop = binbase[(g + 1) * gwords];
+    if (blockIdx.x >= light_blocks) {
+        heavy_slices<F>(chunk_off, partials, buckets, H, blockIdx.x - light_blocks, gridDim.x - light_blocks);
+        return;
+    }
+    const uint32_t start = binbase[0], stop = binbase[gwords];
     const uint32_t t = start + (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
     if (t >= stop) return;
     const uint32_t b = perm[t];
@@ -315,17 +344,6 @@ __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32
     if (k1 > k0) acc = load_jac<L>(partials, k0);
     for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<L>(partials, k));
     store_jac<L>(buckets, b, acc);
-}
-
-template <class F>
-__global__ __launch_bounds__(256) void k_bucket_gather(const uint32_t* __restrict__ chunk_off, uint32_t b0, uint32_t b1,
-                                                       const uint32_t* __restrict__ maxc,
-                                                       const uint8_t* __restrict__ partials, uint8_t* __restrict__ buckets) {
-    if (*maxc <= SMALL_MAX) return;
-    uint32_t b = b0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= b1) return;
-    const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
-    if (k1 - k0 > SMALL_MAX) store_jac<F>(buckets, b, load_jac<F>(partials, k0));
 }
 
 // ------------------------------------------------------------------------------------
@@ -399,109 +417,57 @@ struct RedIO<F, MODE_WAVE> {
 template <int MODE>
 constexpr uint32_t lanes_per_chain() { return MODE == MODE_LANE ? 1u : MODE == MODE_ROW ? 16u : 64u; }
 
+// Scaled running-sum level: every level's outputs carry weight 1, so
+// the last level's single output per window IS the window sum -- no per-level T tree sums on side
+// streams and no window Horner.  Level l sees inputs with
+//   G_w = sum_k ((k + off) V_k + U_k)            (level 0: V = buckets, off = 1, no U)
+// and segment q = [k0, k1) of 2^s inputs produces
+//   U'_q = sum_t (t - k0 + off) V_t + sum_t U_t   (running sum: R += V_t; S += R; S += U_t)
+//   V'_q = 2^s sum_t V_t                           (s doublings of R)
+// so that G_w = sum_q (q V'_q + U'_q): the same form with off = 0.  One add call site (the three
+// steps of a t alternate), one doubling call site.
 template <class F, int MODE>
-__global__ __launch_bounds__(256) void k_reduce_level(const uint8_t* __restrict__ V, uint32_t m_in, uint32_t seg, int Wg,
-                                                      int off, uint8_t* __restrict__ T, uint8_t* __restrict__ R) {
+__global__ __launch_bounds__(256) void k_reduce_scaled(const uint8_t* __restrict__ V, const uint8_t* __restrict__ U,
+                                                       uint32_t m_in, uint32_t seg_log, int Wg, int off,
+                                                       uint8_t* __restrict__ Vout, uint8_t* __restrict__ Uout) {
     MBLS_TAIL_PRIO();
     using IO = RedIO<F, MODE>;
     using J = typename IO::J;
-    const uint32_t m_out = (m_in + seg - 1) / seg;
+    const uint32_t seg = 1u << seg_log;
+    const uint32_t m_out = (m_in + seg - 1) >> seg_log;
     const uint32_t tid = IO::id();
     if (tid >= m_out * (uint32_t)Wg) return;
     const uint32_t w = tid / m_out, q = tid % m_out;
-    const uint32_t k0 = q * seg;
+    const uint32_t k0 = q << seg_log;
     const uint32_t k1 = min(k0 + seg, m_in);  // exclusive
-    J Racc = J::inf(), Sacc = J::inf();
-    // walk t = k1-1 .. k0: R += V_t; S += R unless (t - k0 + off) == 0
-    int steps = 2 * (int)(k1 - k0);
+    const size_t base = (size_t)w * m_in;
+    J R = J::inf(), S = J::inf();
     uint32_t t = k1 - 1;
-    for (int s = 0; s < steps; ++s) {
-        const bool r_step = (s & 1) == 0;
-        if (!r_step && (t - k0) + off == 0) {
+    int ph = 0;  // 0: R += V_t, 1: S += R, 2: S += U_t
+    while (true) {
+        const bool skip = (ph == 1 && (t - k0) + off == 0) || (ph == 2 && !U);
+        if (!skip) {
+            const J x = ph == 0 ? R : S;
+            const J y = ph == 0 ? IO::ld(V, base + t) : ph == 1 ? R : IO::ld(U, base + t);
+            const J z = IO::add(x, y);
+            if (ph == 0)
+                R = z;
+            else
+                S = z;
+        }
+        if (ph == 2) {
             if (t == k0) break;
             --t;
-            continue;
-        }
-        J x = r_step ? Racc : Sacc;
-        J y = r_step ? IO::ld(V, (size_t)w * m_in + t) : Racc;
-        J z = IO::add(x, y);
-        if (r_step) {
-            Racc = z;
+            ph = 0;
         } else {
-            Sacc = z;
-            if (t == k0) break;
-            --t;
+            ++ph;
         }
     }
-    IO::st(T, tid, Sacc);
-    IO::st(R, tid, Racc);
-}
-
-// tree-sum stage: block b of window w sums V[w*m + k], k in [b*16*per_row, ...): each of the
-// 16 rows sums `per_row` consecutive points, then a 4-level LDS tree.  out[w*nblk + b].
-#ifndef MBLS_TREE_PER_ROW
-#define MBLS_TREE_PER_ROW 2  // 8 / 4 / 2: G2 2^20 12.81 / 12.66 / 12.64 ms, G1 reduction 1.02 / 1.01 / 1.00 ms
-#endif
-static constexpr int TREE_PER_ROW = MBLS_TREE_PER_ROW;
-template <class F>
-MBLS_DEV void tree_sum_block(const uint8_t* __restrict__ V, uint32_t m, uint32_t w, uint32_t blk, uint32_t per_row,
-                             uint8_t* __restrict__ out, uint32_t out_idx) {
-    __shared__ __attribute__((aligned(16))) uint8_t sh[16 * 3 * sizeof(F)];
-    const uint32_t r = threadIdx.x >> 4;  // row in block
-    RJac<F> acc = RJac<F>::inf();
-    const uint32_t k0 = (blk * 16 + r) * per_row;
-    for (uint32_t k = k0; k < min(k0 + per_row, m); ++k) acc = jac_add(acc, rload_jac<F>(V, (size_t)w * m + k));
-    rstore_jac<F>(sh, r, acc);
-    __syncthreads();
-    for (uint32_t s = 8; s > 0; s >>= 1) {
-        if (r < s) {
-            acc = jac_add(acc, rload_jac<F>(sh, r + s));
-            rstore_jac<F>(sh, r, acc);
-        }
-        __syncthreads();
+    if (Vout) {
+        for (uint32_t k = 0; k < seg_log; ++k) R = IO::dbl(R);
+        IO::st(Vout, tid, R);
     }
-    if (r == 0) rstore_jac<F>(out, out_idx, acc);
-}
-
-template <class F>
-__global__ __launch_bounds__(256) void k_tree_sum(const uint8_t* __restrict__ V, uint32_t m, uint32_t nblk,
-                                                  uint8_t* __restrict__ out) {
-    MBLS_TAIL_PRIO();
-    tree_sum_block<F>(V, m, blockIdx.x / nblk, blockIdx.x % nblk, TREE_PER_ROW, out, blockIdx.x);
-}
-
-// the narrowest levels' T sums (<= 2 points per row), all in one launch after the last level:
-// block (job, window), ceil(m / 16) points per row then the 4-level LDS tree.  Forked per level
-// they queued behind the wide levels' trees on the side streams (~90 us each).
-static constexpr uint32_t TREE_DEFER_POINTS = 32;
-static constexpr int TREE_SIDES = 3;  // side streams for the wide levels' trees (round robin)
-struct TreeJobs {
-    const uint8_t* V[MAX_LEVELS];
-    uint8_t* out[MAX_LEVELS];
-    uint32_t m[MAX_LEVELS];
-};
-template <class F>
-__global__ __launch_bounds__(256) void k_tree_sum_jobs(TreeJobs jobs, int Wg) {
-    MBLS_TAIL_PRIO();
-    const uint32_t j = blockIdx.x / Wg, w = blockIdx.x % Wg;
-    tree_sum_block<F>(jobs.V[j], jobs.m[j], w, 0, (jobs.m[j] + 15) / 16, jobs.out[j], w);
-}
-
-// G_w = sumT[0] + seg_0*(sumT[1] + seg_1*(sumT[2] + ...)): sums[l * Wg + w]; one chain per window
-template <class F, int MODE>
-__global__ void k_window_horner(const uint8_t* __restrict__ sums, int levels, int Wg, uint64_t seg_logs,
-                                uint8_t* __restrict__ windows) {
-    MBLS_TAIL_PRIO();
-    using IO = RedIO<F, MODE>;
-    const int w = (int)IO::id();
-    if (w >= Wg) return;
-    auto acc = IO::ld(sums, (size_t)(levels - 1) * Wg + w);
-    for (int l = levels - 2; l >= 0; --l) {
-        const int dbls = (int)((seg_logs >> (4 * l)) & 15);
-        for (int k = 0; k < dbls; ++k) acc = IO::dbl(acc);
-        acc = IO::add(acc, IO::ld(sums, (size_t)l * Wg + w));
-    }
-    IO::st(windows, w, acc);
+    IO::st(Uout, tid, S);
 }
 
 // final fold over window groups: sum_w 2^(c w) G_w  (one chain)
@@ -705,24 +671,15 @@ struct GroupTraits<Fq2> {
 };
 
 struct MsmScratchSizes {
-    size_t dsrc, keys, vals, ranks, sorted, words, tmp, owner, first, partials, buckets, levelT, levelR, sums, windows, treetmp, phi;
+    size_t dsrc, keys, vals, ranks, sorted, words, tmp, owner, first, partials, buckets, levelT, levelR, windows, phi;
     size_t ent, segtab, parts;  // partitioned sort (keys / vals / ranks are 0 then)
     size_t order, perm;         // k_bucket_order: bin histograms / their scan, bucket permutation
+    size_t heavy, hslices, hres;  // HeavyTab: per-entry words (x4), per-slice owner words, slice sums
     size_t total() const {
-        return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + first + partials + buckets + levelT + levelR + sums + windows +
-               2 * TREE_SIDES * treetmp + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm;
+        return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + first + partials + buckets + levelT + levelR +
+               windows + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm + 4 * heavy + hslices + hres;
     }
 };
-
-// narrow levels' T sums batched into one launch after the last level (MBLS_DEFER_TREES=0: per
-// level on the side stream)
-inline bool defer_narrow_trees() {
-    static const bool v = [] {
-        const char* e = getenv("MBLS_DEFER_TREES");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
 
 // reduction levels with fewer segments than this run one segment per wave (MBLS_WAVE_MIN tunes;
 // G2: MBLS_WAVE_MIN_G2).  An Fq2 row-sliced addition is three row products per Fq2 product in
@@ -739,7 +696,6 @@ inline uint32_t wave_min_chains(bool fq2 = false) {
     }();
     return fq2 ? v2 : v;
 }
-inline uint32_t tree_blocks(uint32_t m) { return (m + 16 * TREE_PER_ROW - 1) / (16 * TREE_PER_ROW); }
 
 inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks) {
     MsmScratchSizes z;
@@ -759,7 +715,14 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     }
     z.dsrc = align_up(digits_src_bytes((uint32_t)(P.split > 1 ? P.pts / P.split : P.pts / P.F), P.split));
     z.sorted = align_up(NC * 4);
-    z.words = align_up(((size_t)P.TB + 1) * 4);
+    z.words = align_up(((size_t)P.TB + 4) * 4);  // + the maximum and the HeavyTab counters
+    // heavy buckets have > SMALL_MAX partials: at most max_chunks / (SMALL_MAX + 1) of them, and
+    // at most max_chunks / HEAVY_SLICE + (heavy buckets) slices
+    const size_t max_heavy = std::min<size_t>(P.TB, max_chunks / (SMALL_MAX + 1) + 1);
+    const size_t max_slices = max_chunks / HEAVY_SLICE + max_heavy + 1;
+    z.heavy = align_up(max_heavy * 4);
+    z.hslices = align_up(max_slices * 4);
+    z.hres = align_up(max_slices * jac);
     z.order = align_up(((size_t)order_words(P.TB) + 1) * 4);
     z.perm = align_up((size_t)P.TB * 4);
     // + the chunk-count block totals and their prefixes (k_chunk_counts / k_scan_small)
@@ -770,17 +733,11 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     z.first = align_up((NC / P.chunk + 2) * 4);
     z.partials = align_up((size_t)max_chunks * jac);
     z.buckets = align_up((size_t)P.TB * jac);
-    size_t lv = 0, maxblk = 1;
-    for (int l = 0; l < P.levels; ++l) {
-        uint32_t mo = (P.level_m[l] + P.seg(l) - 1) / P.seg(l);
-        lv += mo;
-        maxblk = maxblk > tree_blocks(mo) ? maxblk : tree_blocks(mo);
-    }
-    z.levelT = align_up(lv * P.Wg * jac);
-    z.levelR = align_up(lv * P.Wg * jac);
-    z.sums = align_up((size_t)P.levels * P.Wg * jac);
+    // V / U ping-pong halves sized for the widest level's outputs (k_reduce_scaled)
+    const size_t mo0 = P.levels ? (P.level_m[0] + P.seg(0) - 1) / P.seg(0) : 1;
+    z.levelT = align_up(2 * mo0 * P.Wg * jac);
+    z.levelR = align_up(2 * mo0 * P.Wg * jac);
     z.windows = align_up((size_t)P.Wg * jac);
-    z.treetmp = align_up(maxblk * P.Wg * jac);
     return z;
 }
 
@@ -844,18 +801,18 @@ inline uint32_t accumulate_chunk(const MsmPlan& P) {
 
 // one reduction level over Wl windows (weights t + off; off = 1 at level 0: bucket t holds digit t + 1)
 template <class F>
-inline void launch_reduce_level(int mode, const uint8_t* V, uint32_t m_in, uint32_t seg, int Wl, int off, uint8_t* T,
-                                uint8_t* R, uint32_t chains, hipStream_t s) {
+inline void launch_reduce_scaled(int mode, const uint8_t* V, const uint8_t* U, uint32_t m_in, uint32_t seg_log, int Wl,
+                                 int off, uint8_t* Vo, uint8_t* Uo, uint32_t chains, hipStream_t s) {
     constexpr uint32_t LN = LaneOf<F>::LANES;
-    if (mode == MODE_LANE)  // one segment per lane
-        hipLaunchKernelGGL((k_reduce_level<F, MODE_LANE>), dim3((chains * LN + 255) / 256), dim3(256), 0, s, V, m_in, seg,
-                           Wl, off, T, R);
-    else if (mode == MODE_ROW)  // many segments: one per 16-lane row
-        hipLaunchKernelGGL((k_reduce_level<F, MODE_ROW>), dim3((chains * 16 + 255) / 256), dim3(256), 0, s, V, m_in, seg,
-                           Wl, off, T, R);
-    else  // few segments: one per wave (latency-bound chains)
-        hipLaunchKernelGGL((k_reduce_level<F, MODE_WAVE>), dim3((chains * 64 + 255) / 256), dim3(256), 0, s, V, m_in, seg,
-                           Wl, off, T, R);
+    if (mode == MODE_LANE)
+        hipLaunchKernelGGL((k_reduce_scaled<F, MODE_LANE>), dim3((chains * LN + 255) / 256), dim3(256), 0, s, V, U, m_in,
+                           seg_log, Wl, off, Vo, Uo);
+    else if (mode == MODE_ROW)
+        hipLaunchKernelGGL((k_reduce_scaled<F, MODE_ROW>), dim3((chains * 16 + 255) / 256), dim3(256), 0, s, V, U, m_in,
+                           seg_log, Wl, off, Vo, Uo);
+    else
+        hipLaunchKernelGGL((k_reduce_scaled<F, MODE_WAVE>), dim3((chains * 64 + 255) / 256), dim3(256), 0, s, V, U, m_in,
+                           seg_log, Wl, off, Vo, Uo);
 }
 
 // Core MSM on device operands: scalars (standard or Montgomery), bases Montgomery affine
@@ -896,11 +853,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint8_t* buckets = (uint8_t*)arena.take(z.buckets);
     uint8_t* levelT = (uint8_t*)arena.take(z.levelT);
     uint8_t* levelR = (uint8_t*)arena.take(z.levelR);
-    uint8_t* sums = (uint8_t*)arena.take(z.sums);
     uint8_t* windows = (uint8_t*)arena.take(z.windows);
-    uint8_t* tree_tmp[TREE_SIDES][2];
-    for (int k = 0; k < TREE_SIDES; ++k)
-        for (int h = 0; h < 2; ++h) tree_tmp[k][h] = (uint8_t*)arena.take(z.treetmp);
     uint8_t* phi = P.split > 1 ? (uint8_t*)arena.take(z.phi) : nullptr;
     const bool psort = partition_sort(P);
     uint32_t* ent = (uint32_t*)arena.take(z.ent);
@@ -911,16 +864,22 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint32_t* binhist = (uint32_t*)arena.take(z.order);
     uint32_t* binbase = (uint32_t*)arena.take(z.order);
     uint32_t* perm = (uint32_t*)arena.take(z.perm);
-    if (!perm || !tree_tmp[TREE_SIDES - 1][1] || (P.split > 1 && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
+    HeavyTab H;
+    H.bucket = (uint32_t*)arena.take(z.heavy);
+    H.first = (uint32_t*)arena.take(z.heavy);
+    H.nslices = (uint32_t*)arena.take(z.heavy);
+    H.done = (uint32_t*)arena.take(z.heavy);
+    H.owner = (uint32_t*)arena.take(z.hslices);
+    H.res = (uint8_t*)arena.take(z.hres);
+    H.cnt = nchunks + TB + 1;
+    if (!H.res || !windows || (P.split > 1 && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
-    // side streams: the endomorphism table and the heavy-bucket passes overlap the main chain;
-    // the per-level tree sums of the reduction run there too.  events: [0, levels] tree forks /
-    // join, then [levels + 1, + 4 + TREE_SIDES) table / heavy / joins
-    if ((er = ctx.ensure_side((size_t)P.levels + 5 + TREE_SIDES, TREE_SIDES)) != MBLS_SUCCESS) return er;
+    // side stream: the endomorphism table overlaps the digit / sort front (fork ev[0], join ev[1])
+    if ((er = ctx.ensure_side(2, 1)) != MBLS_SUCCESS) return er;
     hipStream_t side = ctx.sides[0];
-    hipEvent_t* ev = ctx.events.data() + P.levels + 1;
+    hipEvent_t* ev = ctx.events.data();
     if (P.split > 1) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
         MBLS_TRY(hipEventRecord(ev[0], st));
         MBLS_TRY(hipStreamWaitEvent(side, ev[0], 0));
@@ -958,11 +917,9 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         if ((er = launch_order_scan(binhist, binbase, TB, blk_tot, blk_pre, st)) != MBLS_SUCCESS) return er;
         if (!psort && (er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
         if ((er = launch_chunk_owner(cloc, blk_pre, chunk_off, offsets, TB, P.chunk, owner, first, nchunks, binbase,
-                                     1u, perm, st)) != MBLS_SUCCESS)
+                                     perm, H, st)) != MBLS_SUCCESS)
             return er;
     }
-    // worst case: every contribution of a window in one bucket
-    const uint32_t max_per_bucket = (uint32_t)((P.pts + P.chunk - 1) / P.chunk);
     const uint32_t nsplit = P.split > 1 ? n : 0xffffffffu;
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
@@ -974,85 +931,34 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     }
     {
         ProfScope ps("msm.bucket_sum", st);
-        // heavy buckets (> SMALL_MAX chunks; no-op passes for random inputs) on the side stream,
-        // concurrently with the light ones: disjoint partials / buckets
-        static const bool skip_heavy = getenv("MBLS_DIAG_SKIP_HEAVY") != nullptr;  // TEMP timing probe
-        if (max_per_bucket > SMALL_MAX && !skip_heavy) {
-            MBLS_TRY(hipEventRecord(ev[2], st));
-            MBLS_TRY(hipStreamWaitEvent(side, ev[2], 0));
-            for (uint32_t step = 1; step < max_per_bucket; step *= TREE_FANIN)
-                hipLaunchKernelGGL(k_bucket_tree<F>, dim3(std::min((max_chunks * LN + 255) / 256, (uint32_t)MBLS_HEAVY_GRID)),
-                                   dim3(256), 0, side, chunk_off, owner, 0u, TB, max_chunks, nchunks + TB, step, partials);
-            hipLaunchKernelGGL(k_bucket_gather<F>, dim3((TB + 255) / 256), dim3(256), 0, side, chunk_off, 0u, TB,
-                               nchunks + TB, partials, buckets);
-            MBLS_TRY(hipEventRecord(ev[3], side));
-        }
-        hipLaunchKernelGGL(k_bucket_small<F>, dim3((TB * LN + 255) / 256), dim3(256), 0, st, chunk_off, perm, binbase,
-                           0u, order_words(TB), partials, buckets);
-        if (max_per_bucket > SMALL_MAX && !skip_heavy) MBLS_TRY(hipStreamWaitEvent(st, ev[3], 0));
+        // light buckets one thread each, heavy buckets by slice workgroups in the same launch
+        // (k_bucket_small); forked heavy passes on a side stream cost ~20 us per event wait,
+        // in-line empty passes ~6 us per launch (round 3 timelines)
+        const uint32_t light_blocks = (TB * LN + 255) / 256;
+        hipLaunchKernelGGL(k_bucket_small<F>, dim3(light_blocks + HEAVY_BLOCKS), dim3(256), 0, st, chunk_off, perm, binbase,
+                           order_words(TB), partials, buckets, light_blocks, H);
     }
     ProfScope ps_red("msm.reduce", st);
-    // recursive running-sum reduction.  The per-level T tree sums are latency-bound chains off
-    // the critical path: they run on the context's side streams, forked after each level and
-    // joined before the window Horner.
-    const uint8_t* V = buckets;
-    size_t lvoff = 0;
-    TreeJobs jobs;
-    int njobs = 0, ntree = 0;
-    bool used[TREE_SIDES] = {};
-    for (int l = 0; l < P.levels; ++l) {
-        const uint32_t m_in = P.level_m[l];
-        const uint32_t seg = P.seg(l);
-        const uint32_t m_out = (m_in + seg - 1) / seg;
-        uint8_t* T = levelT + lvoff * JAC;
-        uint8_t* R = levelR + lvoff * JAC;
-        const uint32_t chains = m_out * (uint32_t)P.Wg;
-        launch_reduce_level<F>(P.mode[l], V, m_in, seg, P.Wg, l == 0 ? 1 : 0, T, R, chains, st);
-        // sum of this level's T per window: narrow levels are batched after the last level;
-        // wide ones run tree stages on a side stream, overlapped with the next levels
-        if (m_out <= TREE_DEFER_POINTS && defer_narrow_trees()) {
-            jobs.V[njobs] = T;
-            jobs.m[njobs] = m_out;
-            jobs.out[njobs] = sums + (size_t)l * P.Wg * JAC;
-            ++njobs;
-            V = R;
-            lvoff += (size_t)m_out * P.Wg;
-            continue;
+    {
+        // scaled running-sum levels (k_reduce_scaled): V / U ping-pong in levelR / levelT, the
+        // last level writes the window sums straight into `windows`
+        const size_t half = ((P.level_m[0] + P.seg(0) - 1) / P.seg(0)) * (size_t)P.Wg * JAC;
+        uint8_t* vb[2] = {levelR, levelR + half};
+        uint8_t* ub[2] = {levelT, levelT + half};
+        const uint8_t* V = buckets;
+        const uint8_t* U = nullptr;
+        for (int l = 0; l < P.levels; ++l) {
+            const uint32_t m_in = P.level_m[l];
+            const uint32_t m_out = (m_in + P.seg(l) - 1) / P.seg(l);
+            const bool last = l == P.levels - 1;
+            uint8_t* Vo = last ? nullptr : vb[l & 1];
+            uint8_t* Uo = last ? windows : ub[l & 1];
+            launch_reduce_scaled<F>(P.mode[l], V, U, m_in, P.seg_log[l], P.Wg, l == 0 ? 1 : 0, Vo, Uo,
+                                    m_out * (uint32_t)P.Wg, st);
+            V = Vo;
+            U = Uo;
         }
-        const int sk = ntree++ % TREE_SIDES;
-        hipStream_t ts = ctx.sides[sk];
-        used[sk] = true;
-        MBLS_TRY(hipEventRecord(ctx.events[l], st));
-        MBLS_TRY(hipStreamWaitEvent(ts, ctx.events[l], 0));
-        const uint8_t* src = T;
-        uint32_t m = m_out;
-        uint8_t** pp = tree_tmp[sk];
-        int flip = 0;
-        while (true) {
-            const uint32_t nblk = tree_blocks(m);
-            uint8_t* dst = (nblk == 1) ? sums + (size_t)l * P.Wg * JAC : pp[flip];
-            hipLaunchKernelGGL(k_tree_sum<F>, dim3(P.Wg * nblk), dim3(256), 0, ts, src, m, nblk, dst);
-            if (nblk == 1) break;
-            src = dst;
-            m = nblk;
-            flip ^= 1;
-        }
-        V = R;
-        lvoff += (size_t)m_out * P.Wg;
     }
-    if (njobs) hipLaunchKernelGGL(k_tree_sum_jobs<F>, dim3(njobs * P.Wg), dim3(256), 0, st, jobs, P.Wg);
-    // join the side streams (the first also carried the table / heavy-bucket work): the others
-    // fold into side 0, so the main stream waits once (each wait on it is a barrier packet,
-    // ~5 us of gap ahead of the window Horner)
-    for (int k = 1; k < TREE_SIDES; ++k) {
-        if (!used[k]) continue;
-        MBLS_TRY(hipEventRecord(ev[3 + k], ctx.sides[k]));
-        MBLS_TRY(hipStreamWaitEvent(ctx.sides[0], ev[3 + k], 0));
-    }
-    MBLS_TRY(hipEventRecord(ctx.events[P.levels], ctx.sides[0]));
-    MBLS_TRY(hipStreamWaitEvent(st, ctx.events[P.levels], 0));
-    hipLaunchKernelGGL((k_window_horner<F, MODE_WAVE>), dim3(P.Wg), dim3(64), 0, st, sums, P.levels, P.Wg,
-                       P.seg_logs_packed(), windows);
     {
         ProfScope ps("msm.final", st);
         if (icicle_out)

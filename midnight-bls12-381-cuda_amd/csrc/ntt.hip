@@ -35,10 +35,22 @@
 
 namespace mbls {
 
-static constexpr int NTT_TILE_LOG = 10;
+#ifndef MBLS_NTT_TILE_LOG
+#define MBLS_NTT_TILE_LOG 10
+#endif
+#ifndef MBLS_NTT_PASS_STAGES
+#define MBLS_NTT_PASS_STAGES 8
+#endif
+#ifndef MBLS_NTT_THREADS
+#define MBLS_NTT_THREADS 256
+#endif
+#ifndef MBLS_NTT_XCD
+#define MBLS_NTT_XCD 0  // 1: tiles of adjacent columns on the same XCD (shared L2 lines)
+#endif
+static constexpr int NTT_TILE_LOG = MBLS_NTT_TILE_LOG;
 static constexpr int NTT_TILE = 1 << NTT_TILE_LOG;  // elements per workgroup tile
-static constexpr int NTT_THREADS = 256;
-static constexpr int NTT_PASS_STAGES = 8;
+static constexpr int NTT_THREADS = MBLS_NTT_THREADS;
+static constexpr int NTT_PASS_STAGES = MBLS_NTT_PASS_STAGES;
 
 // canonical 2^32-th root of unity, Montgomery (bls12_381_constants.h:127-130)
 static const uint64_t ROOT_2_32_MONT[4] = {0xb9b58d8c5f0e466aULL, 0x5b1b4c801819d7ecULL, 0x0af53ae352a31e64ULL,
@@ -166,8 +178,10 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ 
     const int T = rows * C;  // active tile elements (== NTT_TILE except for tiny transforms)
     const size_t n = (size_t)1 << log_n;
     const int tiles_per_poly = (int)(n >> (L + logC));
-    const int poly = blockIdx.x / tiles_per_poly;
-    const int tile = blockIdx.x % tiles_per_poly;
+    int bid = (int)blockIdx.x;
+    if (MBLS_NTT_XCD && (gridDim.x & 7) == 0) bid = (bid & 7) * (int)(gridDim.x >> 3) + (bid >> 3);
+    const int poly = bid / tiles_per_poly;
+    const int tile = bid % tiles_per_poly;
     const size_t pbase = (size_t)poly * n;
 
     // ---- load tile into LDS as [row t][col c]

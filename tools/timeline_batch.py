@@ -7,5 +7,5 @@ for r in rows:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     if s < t0: continue
     n = r["Kernel_Name"].split("(")[0].replace("void ","").replace("mbls::","")[:34]
-    if any(k in n for k in ("k_accumulate", "k_bucket_small", "k_reduce_level", "k_final", "k_digits_part", "k_part_sort", "k_jac")):
+    if any(k in n for k in ("k_accumulate", "k_bucket_small", "k_reduce_scaled", "k_final", "k_digits_part", "k_part_sort", "k_jac")):
         print(f"{(s-t0)/1e3:9.1f} {(e-s)/1e3:8.1f} q{r.get('Queue_Id','?'):>3} {n}")
