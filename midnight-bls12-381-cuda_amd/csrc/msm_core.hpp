@@ -224,9 +224,8 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
         };
         issue(v, 0);
         uint32_t vn = beg + 1 < end ? sorted[beg + 1] : v;
-        uint32_t it = 0;
-        for (uint32_t e = beg; e < end; ++e, ++it) {
-            const uint32_t slot = it & 1;
+        for (uint32_t e = beg; e < end; ++e) {
+            const uint32_t slot = (e - beg) & 1;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this point's pieces have landed
             Affine<Fq> p;
 #pragma unroll
@@ -684,7 +683,8 @@ struct MsmScratchSizes {
 // reduction levels with fewer segments than this run one segment per wave (MBLS_WAVE_MIN tunes;
 // G2: MBLS_WAVE_MIN_G2).  An Fq2 row-sliced addition is three row products per Fq2 product in
 // series, so G2 switches to the wave layout (the three spread over rows) at more segments
-// (4096, with G2 row segments of 8: msm_common.hip plan_levels).
+// (8192, with G2 row segments of 8: msm_common.hip plan_levels; 4096 measured 1.75 ms of G2
+// reduction at 2^20, 8192 and 16384 1.64 ms).
 inline uint32_t wave_min_chains(bool fq2 = false) {
     static const uint32_t v = [] {
         const char* e = getenv("MBLS_WAVE_MIN");
@@ -692,7 +692,7 @@ inline uint32_t wave_min_chains(bool fq2 = false) {
     }();
     static const uint32_t v2 = [] {
         const char* e = getenv("MBLS_WAVE_MIN_G2");
-        return e ? (uint32_t)atoi(e) : 4096u;
+        return e ? (uint32_t)atoi(e) : 8192u;
     }();
     return fq2 ? v2 : v;
 }
