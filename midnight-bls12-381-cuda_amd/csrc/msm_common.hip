@@ -26,8 +26,17 @@ static int optimal_c(long long n) {
 
 int precompute_shift(int F) { return F > 1 ? (256 + F - 1) / F : 0; }
 
+// MBLS_C=<c> overrides the automatic window size (tuning sweeps; the caller's c wins)
+static int auto_c(long long n) {
+    static const int v = [] {
+        const char* e = getenv("MBLS_C");
+        return e ? atoi(e) : 0;
+    }();
+    return v >= 2 && v <= 20 ? v : optimal_c(n);
+}
+
 eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) {
-    int c = cfg->c > 0 ? cfg->c : optimal_c(n);
+    int c = cfg->c > 0 ? cfg->c : auto_c(n);
     if (c < 2 || c > 20) return MBLS_INVALID_ARGUMENT;
     int bits = cfg->bitsize > 0 ? cfg->bitsize : 255;
     if (bits > 256) return MBLS_INVALID_ARGUMENT;

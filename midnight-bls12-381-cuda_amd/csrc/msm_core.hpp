@@ -469,6 +469,99 @@ __global__ __launch_bounds__(256) void k_reduce_scaled(const uint8_t* __restrict
     IO::st(Uout, tid, S);
 }
 
+// A narrow level (few segments: the GPU is idle but for one wave per chain) as a tree: one
+// workgroup of 4 waves per segment of 4 inputs (off = 0), each wave one wave-layout point op per
+// step, intermediate points through LDS.  The same outputs as k_reduce_scaled's chain
+//   U' = V1 + 2 V2 + 3 V3 + U0 + U1 + U2 + U3,   V' = 4 (V0 + V1 + V2 + V3)
+// in 4 dependent steps instead of 12:
+//   1: a = V2 + V3 | b = U0 + U1 | c = U2 + U3 | d = V0 + V1
+//   2: e = a + V3  | k = a + V1  | f = b + c   | g = d + a
+//   3: W = k + e                               | 2g
+//   4: U' = W + f                              | V' = 4g
+// (inputs past the level's end are the identity; the additions are exact point additions, so
+// the association does not change the resulting point -- only its Jacobian representative,
+// which the final (x, y, 1) normalisation removes)
+template <class F>
+struct TreeLds {
+    using J = RJac<F>;
+    static constexpr int FQS = RowOf<F>::FQS;  // Fq words-of-12 per coordinate
+    static constexpr int WORDS = 3 * FQS * 12;
+    MBLS_DEV static void put1(uint32_t* s, const RFq& a) {
+        if (wave::row() == 0 && rowdpp::lane16() < 12) s[rowdpp::lane16()] = a.v;
+    }
+    MBLS_DEV static RFq get1(const uint32_t* s) {
+        const uint32_t j = rowdpp::lane16();
+        return {j < 12 ? s[j] : 0u};
+    }
+    MBLS_DEV static void put1(uint32_t* s, const RFq2& a) {
+        put1(s, a.c0);
+        put1(s + 12, a.c1);
+    }
+    MBLS_DEV static void get1(const uint32_t* s, RFq2& a) {
+        a.c0 = get1(s);
+        a.c1 = get1(s + 12);
+    }
+    MBLS_DEV static void get1(const uint32_t* s, RFq& a) { a = get1(s); }
+    MBLS_DEV static void put(uint32_t* s, const J& p) {
+        put1(s, p.x);
+        put1(s + 12 * FQS, p.y);
+        put1(s + 24 * FQS, p.z);
+    }
+    MBLS_DEV static J get(const uint32_t* s) {
+        J p;
+        get1(s, p.x);
+        get1(s + 12 * FQS, p.y);
+        get1(s + 24 * FQS, p.z);
+        return p;
+    }
+};
+
+template <class F>
+__global__ __launch_bounds__(256) void k_reduce_tree4(const uint8_t* __restrict__ V, const uint8_t* __restrict__ U,
+                                                      uint32_t m_in, uint8_t* __restrict__ Vout,
+                                                      uint8_t* __restrict__ Uout) {
+    MBLS_TAIL_PRIO();
+    using IO = RedIO<F, MODE_WAVE>;
+    using J = RJac<F>;
+    using T = TreeLds<F>;
+    __shared__ uint32_t slot[8][T::WORDS];
+    const uint32_t m_out = (m_in + 3) >> 2;
+    const uint32_t seg = blockIdx.x;  // grid = m_out * windows exactly
+    const uint32_t w = seg / m_out, q = seg % m_out;
+    const uint32_t k0 = q << 2, cnt = min(4u, m_in - k0);
+    const size_t base = (size_t)w * m_in + k0;
+    const int wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    auto ldV = [&](uint32_t t) { return t < cnt ? IO::ld(V, base + t) : J::inf(); };
+    auto ldU = [&](uint32_t t) { return (U && t < cnt) ? IO::ld(U, base + t) : J::inf(); };
+    J r = J::inf();
+    // steps 1..3 of the additions share one call site (wave-uniform operand selection)
+    for (int step = 0; step < 3; ++step) {
+        const bool active = step < 2 || wv == 0;
+        J x = J::inf(), y = J::inf();
+        if (step == 0) {
+            x = wv == 0 ? ldV(2) : wv == 1 ? ldU(0) : wv == 2 ? ldU(2) : ldV(0);
+            y = wv == 0 ? ldV(3) : wv == 1 ? ldU(1) : wv == 2 ? ldU(3) : ldV(1);
+        } else if (step == 1) {
+            x = wv == 2 ? T::get(slot[1]) : wv == 3 ? T::get(slot[3]) : T::get(slot[0]);
+            y = wv == 0 ? ldV(3) : wv == 1 ? ldV(1) : wv == 2 ? T::get(slot[2]) : T::get(slot[0]);
+        } else if (active) {
+            x = T::get(slot[5]);  // k
+            y = r;                // e
+        }
+        if (active) r = IO::add(x, y);
+        if (step < 2) {
+            T::put(slot[4 * step + wv], r);
+            __syncthreads();
+        }
+    }
+    if (wv == 0) {
+        IO::st(Uout, seg, IO::add(r, T::get(slot[6])));  // U' = W + f
+    } else if (wv == 3 && Vout) {
+        for (int k = 0; k < 2; ++k) r = IO::dbl(r);  // V' = 4 g
+        IO::st(Vout, seg, r);
+    }
+}
+
 // final fold over window groups: sum_w 2^(c w) G_w  (one chain)
 template <class F, int MODE>
 MBLS_DEV auto final_fold(const uint8_t* __restrict__ windows, int Wg, int c) {
@@ -799,11 +892,25 @@ inline uint32_t accumulate_chunk(const MsmPlan& P) {
     return (uint32_t)std::max<size_t>(CHUNK, L);
 }
 
+// wave-layout levels of 4-input segments with at most this many segments run as trees of 4
+// waves (k_reduce_tree4; MBLS_TREE_MAX tunes, 0 disables)
+inline uint32_t tree_max_chains() {
+    static const uint32_t v = [] {
+        const char* e = getenv("MBLS_TREE_MAX");
+        return e ? (uint32_t)atoi(e) : 512u;
+    }();
+    return v;
+}
+
 // one reduction level over Wl windows (weights t + off; off = 1 at level 0: bucket t holds digit t + 1)
 template <class F>
 inline void launch_reduce_scaled(int mode, const uint8_t* V, const uint8_t* U, uint32_t m_in, uint32_t seg_log, int Wl,
                                  int off, uint8_t* Vo, uint8_t* Uo, uint32_t chains, hipStream_t s) {
     constexpr uint32_t LN = LaneOf<F>::LANES;
+    if (mode == MODE_WAVE && seg_log == 2 && off == 0 && chains <= tree_max_chains()) {
+        hipLaunchKernelGGL(k_reduce_tree4<F>, dim3(chains), dim3(256), 0, s, V, U, m_in, Vo, Uo);
+        return;
+    }
     if (mode == MODE_LANE)
         hipLaunchKernelGGL((k_reduce_scaled<F, MODE_LANE>), dim3((chains * LN + 255) / 256), dim3(256), 0, s, V, U, m_in,
                            seg_log, Wl, off, Vo, Uo);
