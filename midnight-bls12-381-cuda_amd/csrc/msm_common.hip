@@ -50,6 +50,18 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     if (endo == 2 && F == 1 && bits > 128) p.split = 2;
     if (endo == 4 && F == 1 && bits > 192 && c <= 16) p.split = 4;
     if (F > MAX_PRECOMPUTE) return MBLS_INVALID_ARGUMENT;
+    // The split halves / quarters are 128 / 64-bit digit streams.  A caller's large c (picked for
+    // 255-bit scalars, e.g. MIDNIGHT_MSM_WINDOW=15) can leave the top window a few bits wide: all
+    // of that window's 2^21 digits (G1 2^20) then fall into a handful of buckets -- one partition
+    // of the sort and a few heavy buckets take the whole window (c = 15: sort 3.3 ms instead of
+    // 0.16).  c only shapes the schedule, never the result, so c >= 14 whose top window would be
+    // more than 2 bits short becomes 16, which divides both widths (c > 16 also leaves the
+    // partitioned sort).
+    if (p.split > 1 && c >= 14) {
+        const int H = p.split == 2 ? 128 : 64;
+        const int Wc = (H + c - 1) / c;
+        if (H - c * (Wc - 1) < c - 2 || c > 16) c = 16;
+    }
     // signed digits need one bit of headroom for the top carry
     int W = p.split == 2 ? (128 + c - 1) / c : p.split == 4 ? (64 + c - 1) / c : (bits + 1 + c - 1) / c;
     int Wg = W;
@@ -569,6 +581,33 @@ __global__ __launch_bounds__(256) void k_glv_split(const uint8_t* __restrict__ s
     out[n + i] = make_uint4(m2[0], m2[1], m2[2], m2[3] | (n2 ? 0x80000000u : 0u));
 }
 
+// G1 front in one launch: thread i splits scalar i (k_glv_split) AND writes phi(P_i) (k_glv_table)
+// -- the table no longer runs on a side stream beside the digit / sort front (its fork / join
+// event waits and its contention with k_glv_split cost more than its own time)
+template <bool MONT>
+__global__ __launch_bounds__(256) void k_glv_prep(const uint8_t* __restrict__ scalars, uint32_t n,
+                                                  uint4* __restrict__ out, ZeroList z,
+                                                  const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    z.run(i, gridDim.x * blockDim.x);
+    if (i >= n) return;
+    {
+        Affine<Fq> p = load_affine<Fq>(bases, i);
+        Fq beta;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) beta.v[k] = GLV_BETA_MONT[k];
+        p.x = p.x * beta;
+        store_affine<Fq>(phi, i, p);
+    }
+    Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
+    if (MONT) s = from_mont(s);
+    uint32_t m1[4], m2[4];
+    bool n1, n2;
+    glv_split(s, m1, n1, m2, n2);
+    out[i] = make_uint4(m1[0], m1[1], m1[2], m1[3] | (n1 ? 0x80000000u : 0u));
+    out[n + i] = make_uint4(m2[0], m2[1], m2[2], m2[3] | (n2 ? 0x80000000u : 0u));
+}
+
 __global__ void k_scalars_std(const uint8_t* __restrict__ scalars, uint32_t n, uint8_t* __restrict__ out, ZeroList z) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     z.run(i, gridDim.x * blockDim.x);
@@ -670,9 +709,17 @@ __global__ void k_zero_list(ZeroList z) { z.run(blockIdx.x * blockDim.x + thread
 // the MSM's first kernel also clears the words later kernels accumulate into (ZeroList): a
 // separate hipMemsetAsync is a fill kernel of its own, ~9-18 us on the critical path each
 static eIcicleError digit_sources(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint8_t* dsrc,
-                                  const ZeroList& z, hipStream_t st, const uint32_t*& src, uint32_t& nidx) {
+                                  const ZeroList& z, hipStream_t st, const uint32_t*& src, uint32_t& nidx,
+                                  const uint8_t* bases = nullptr, uint8_t* phi = nullptr) {
     dim3 g((n + 255) / 256);
-    if (P.split == 2) {
+    if (P.split == 2 && phi) {  // split + phi table fused (k_glv_prep)
+        if (mont)
+            hipLaunchKernelGGL(k_glv_prep<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi);
+        else
+            hipLaunchKernelGGL(k_glv_prep<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi);
+        src = (const uint32_t*)dsrc;
+        nidx = 2 * n;
+    } else if (P.split == 2) {
         if (mont)
             hipLaunchKernelGGL(k_glv_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);
         else
@@ -1101,7 +1148,7 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
 
 eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* ent,
                                 uint32_t* seg_off, uint32_t* seg_cnt, uint32_t* part_tot, uint8_t* dsrc,
-                                uint32_t* zero_word, hipStream_t st) {
+                                uint32_t* zero_word, hipStream_t st, const uint8_t* bases, uint8_t* phi) {
     if (P.B > DT_MAX_B) return MBLS_INVALID_ARGUMENT;
     const PartSortSizes z = part_sort_sizes(P);
     const uint32_t* src;
@@ -1111,7 +1158,7 @@ eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, c
     zl.n[0] = (uint32_t)P.Wg * z.NP;
     zl.p[1] = zero_word;  // the chunk-count maximum (k_chunk_counts' atomicMax), HeavyTab counters
     zl.n[1] = zero_word ? 3u : 0u;
-    eIcicleError er = digit_sources(scalars, mont, n, P, dsrc, zl, st, src, nidx);
+    eIcicleError er = digit_sources(scalars, mont, n, P, dsrc, zl, st, src, nidx, bases, phi);
     if (er != MBLS_SUCCESS) return er;
     dim3 g(z.segments), b(DT_THREADS);
     const uint32_t F = (uint32_t)P.F;

@@ -139,9 +139,11 @@ struct PartSortSizes {
 };
 bool partition_sort(const MsmPlan& P);
 PartSortSizes part_sort_sizes(const MsmPlan& P);
+// bases / phi (G1 GLV only): the phi table is written by the split kernel itself (k_glv_prep)
 eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* ent,
                                 uint32_t* seg_off, uint32_t* seg_cnt, uint32_t* part_tot, uint8_t* dsrc,
-                                uint32_t* zero_word, hipStream_t st);
+                                uint32_t* zero_word, hipStream_t st, const uint8_t* bases = nullptr,
+                                uint8_t* phi = nullptr);
 eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint32_t* seg_off, const uint32_t* seg_cnt,
                               const uint32_t* part_tot, uint32_t* part_base, uint32_t* tmp, uint32_t* counts,
                               uint32_t* offsets, uint32_t* sorted, hipStream_t st);
@@ -892,6 +894,16 @@ inline uint32_t accumulate_chunk(const MsmPlan& P) {
     return (uint32_t)std::max<size_t>(CHUNK, L);
 }
 
+// G1: the phi table inside the split kernel (k_glv_prep) instead of on a side stream
+// (MBLS_GLV_FUSED=0: side stream, A/B)
+inline bool glv_prep_fused() {
+    static const bool v = [] {
+        const char* e = getenv("MBLS_GLV_FUSED");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 // wave-layout levels of 4-input segments with at most this many segments run as trees of 4
 // waves (k_reduce_tree4; MBLS_TREE_MAX tunes, 0 disables)
 inline uint32_t tree_max_chains() {
@@ -987,7 +999,9 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     if ((er = ctx.ensure_side(2, 1)) != MBLS_SUCCESS) return er;
     hipStream_t side = ctx.sides[0];
     hipEvent_t* ev = ctx.events.data();
-    if (P.split > 1) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
+    // G1 with the partitioned sort: the phi table is written by the split kernel (k_glv_prep)
+    const bool fused_table = P.split == 2 && psort && glv_prep_fused();
+    if (P.split > 1 && !fused_table) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
         MBLS_TRY(hipEventRecord(ev[0], st));
         MBLS_TRY(hipStreamWaitEvent(side, ev[0], 0));
         er = P.split == 2 ? launch_glv_table(bases, phi, n, side) : launch_psi_table(bases, phi, n, side);
@@ -997,7 +1011,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     {
         ProfScope ps("msm.digits", st);
         if (psort) {
-            er = launch_digits_part(scalars, scalars_mont, n, P, ent, seg_off, seg_cnt, part_tot, dsrc, nchunks + TB, st);
+            er = launch_digits_part(scalars, scalars_mont, n, P, ent, seg_off, seg_cnt, part_tot, dsrc, nchunks + TB, st,
+                                    fused_table ? bases : nullptr, fused_table ? phi : nullptr);
         } else {
             MBLS_TRY(hipMemsetAsync(counts, 0, (size_t)TB * 4, st));
             er = launch_digits(scalars, scalars_mont, n, P, keys, vals, ranks, counts, dsrc, st);
@@ -1031,7 +1046,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
         ProfScope ps("msm.accumulate", st);
-        if (P.split > 1) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
+        if (P.split > 1 && !fused_table) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
         const uint32_t threads = (uint32_t)((NC + P.chunk - 1) / P.chunk) * LN;
         hipLaunchKernelGGL(accumulate_kernel<F>(), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
                            chunk_off, first, 0u, TB, bases, phi, nsplit, P.chunk, partials);
@@ -1045,8 +1060,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         hipLaunchKernelGGL(k_bucket_small<F>, dim3(light_blocks + HEAVY_BLOCKS), dim3(256), 0, st, chunk_off, perm, binbase,
                            order_words(TB), partials, buckets, light_blocks, H);
     }
-    ProfScope ps_red("msm.reduce", st);
     {
+        ProfScope ps_red("msm.reduce", st);  // the levels only (k_final has its own scope)
         // scaled running-sum levels (k_reduce_scaled): V / U ping-pong in levelR / levelT, the
         // last level writes the window sums straight into `windows`
         const size_t half = ((P.level_m[0] + P.seg(0) - 1) / P.seg(0)) * (size_t)P.Wg * JAC;

@@ -285,9 +285,17 @@ def test_msm_window_sizes(amd, gh):
     case = [c for c in g["cases"] if c["name"] == "random_300"][0]
     s_std, _, b_mont = _case_arrays(gh, case, "g1")
     expect = H.pt_from_json(case["result"], "g1")
-    for c in (2, 5, 8, 11, 13, 16, 18):
+    for c in (2, 5, 8, 11, 13, 14, 15, 16, 18):  # 14 / 15 / 18 run as 16 with the GLV split
         r = amd.msm("g1", s_std, b_mont, c=c)
         assert gh.decode_icicle("g1", r[0]) == expect, c
+    # c > 16 without a split (G2 keeps the plain 255-bit digits there): the digit + scatter sort
+    g2 = H.load_golden("msm_g2.json")
+    case2 = [c for c in g2["cases"] if c["name"] == "random_64"][0]
+    s2, _, b2 = _case_arrays(gh, case2, "g2")
+    expect2 = H.pt_from_json(case2["result"], "g2")
+    for c in (15, 17, 18):
+        r = amd.msm("g2", s2, b2, c=c)
+        assert gh.decode_icicle("g2", r[0]) == expect2, c
 
 
 def test_msm_points_standard_form(amd, gh):

@@ -22,7 +22,7 @@ ALIASES = (("k_accumulate<mbls::Fp<mbls::FqCfg>", "k_accumulate<G1>"), ("k_accum
            ("k_bucket_small<mbls::Fp<mbls::FqCfg>", "k_bucket_small<G1>"), ("k_bucket_small<mbls::Fq2", "k_bucket_small<G2>"))
 KEYS = ("k_accumulate", "k_ntt_pass<true, false, false>", "k_ntt_pass<false, false, false>",
         "k_ntt_pass<false, true, false>", "k_ntt_pass<false, true, true>", "k_scatter", "k_digits_tiled",
-        "k_digits_part", "k_part_sort", "k_bucket_small", "k_reduce_scaled", "k_glv_table", "k_vecop", "k_final",
+        "k_digits_part", "k_part_sort", "k_bucket_small", "k_reduce_scaled", "k_reduce_tree4", "k_glv_table", "k_glv_prep", "k_vecop", "k_final",
         "k_jac_to_icicle")
 
 

@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 KEEP = ("k_accumulate", "k_ntt_pass", "k_bucket_small", "k_reduce_scaled", "k_final", "k_jac_to_icicle",
-        "k_digits_part", "k_part_sort", "k_glv_table", "k_vecop", "k_glv_split")
+        "k_digits_part", "k_part_sort", "k_glv_table", "k_vecop", "k_glv_split", "k_glv_prep")
 
 
 def short(name):
