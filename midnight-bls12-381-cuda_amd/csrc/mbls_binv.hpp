@@ -83,34 +83,27 @@ MBLS_HD void mul_small(uint32_t (&r)[N + 1], const uint32_t (&a)[N], uint32_t k)
     r[N] = (uint32_t)c;
 }
 
-// S = s_p * P + s_q * Q as sign + magnitude (N+1 words); returns true if negative
+// S = s_p * P + s_q * Q as sign + magnitude (M words, |S| < 2^(32 M - 1)); returns true if
+// negative.  Branch-free (two's complement sum of the conditionally negated operands, then a
+// conditional negation), so the callers' updates stay in one basic block the scheduler can
+// interleave with the next inner loop.
 template <int M>
 MBLS_HD bool signed_sum(uint32_t (&S)[M], const uint32_t (&P)[M], bool np, const uint32_t (&Q)[M], bool nq) {
-    if (np == nq) {
-        uint64_t c = 0;
-        for (int i = 0; i < M; ++i) {
-            c += (uint64_t)P[i] + Q[i];
-            S[i] = (uint32_t)c;
-            c >>= 32;
-        }
-        return np;
-    }
-    int64_t br = 0;
+    const uint32_t mp = np ? ~0u : 0u, mq = nq ? ~0u : 0u;
+    uint64_t c = (uint64_t)(np ? 1u : 0u) + (nq ? 1u : 0u);
     for (int i = 0; i < M; ++i) {
-        int64_t d = (int64_t)P[i] - Q[i] + br;
-        S[i] = (uint32_t)d;
-        br = d >> 32;  // 0 or -1
+        c += (uint64_t)(P[i] ^ mp) + (Q[i] ^ mq);
+        S[i] = (uint32_t)c;
+        c >>= 32;
     }
-    if (br) {  // P < Q: magnitude Q - P, sign of Q
-        uint64_t c = 1;
-        for (int i = 0; i < M; ++i) {
-            c += (uint32_t)~S[i];
-            S[i] = (uint32_t)c;
-            c >>= 32;
-        }
-        return nq;
+    const uint32_t ms = (uint32_t)((int32_t)S[M - 1] >> 31);  // all ones when negative
+    c = ms & 1u;
+    for (int i = 0; i < M; ++i) {
+        c += (uint64_t)(S[i] ^ ms);
+        S[i] = (uint32_t)c;
+        c >>= 32;
     }
-    return np;
+    return ms != 0;
 }
 
 // r = |f a + g b| / 2^K (exact); returns true if f a + g b < 0.  |f|, |g| <= 2^K.
@@ -120,11 +113,15 @@ MBLS_HD bool lincomb_shift(uint32_t (&r)[N], const uint32_t (&a)[N], const uint3
     mul_small<N>(P, a, (uint32_t)(f < 0 ? -f : f));
     mul_small<N>(Q, b, (uint32_t)(g < 0 ? -g : g));
     const bool neg = signed_sum<N + 1>(S, P, f < 0, Q, g < 0);
-    for (int i = 0; i < N; ++i) r[i] = (S[i] >> K) | (S[i + 1] << (32 - K));
-    return neg && !is_zero<N>(r);
+    uint32_t z = 0;
+    for (int i = 0; i < N; ++i) {
+        r[i] = (S[i] >> K) | (S[i + 1] << (32 - K));
+        z |= r[i];
+    }
+    return neg && z != 0;
 }
 
-// r = (f u + g v) / 2^K mod m, u, v in [0, m); result in [0, m).  |f|, |g| <= 2^K.
+// r = (f u + g v) / 2^K mod m, u, v in [0, m); result in [0, m).  |f|, |g| <= 2^K.  Branch-free.
 template <int N>
 MBLS_HD void lincomb_mod(uint32_t (&r)[N], const uint32_t (&u)[N], const uint32_t (&v)[N], int64_t f, int64_t g,
                          const uint32_t (&m)[N], uint32_t ninv) {
@@ -132,14 +129,14 @@ MBLS_HD void lincomb_mod(uint32_t (&r)[N], const uint32_t (&u)[N], const uint32_
     mul_small<N>(P, u, (uint32_t)(f < 0 ? -f : f));
     mul_small<N>(Q, v, (uint32_t)(g < 0 ? -g : g));
     const bool neg = signed_sum<N + 1>(S, P, f < 0, Q, g < 0);
-    if (neg) {  // |S| <= 2^(K+1) m: S <- 2^(K+1) m - |S|, in [0, 2^(K+1) m]
+    {  // negative: |S| <= 2^(K+1) m, S <- 2^(K+1) m - |S| in [0, 2^(K+1) m]
         int64_t br = 0;
         for (int i = 0; i <= N; ++i) {
             const uint32_t lo = i == 0 ? 0u : m[i - 1] >> (31 - K);
             const uint32_t mw = (i < N ? m[i] << (K + 1) : 0u) | lo;
             int64_t d = (int64_t)mw - S[i] + br;
-            S[i] = (uint32_t)d;
             br = d >> 32;
+            S[i] = neg ? (uint32_t)d : S[i];
         }
     }
     // S + k m = 0 (mod 2^K), k = S * (-1/m) mod 2^K; S + k m < 3 * 2^K m < 2^(32(N+1))
@@ -162,14 +159,17 @@ MBLS_HD void lincomb_mod(uint32_t (&r)[N], const uint32_t (&u)[N], const uint32_
             d[i] = (uint32_t)x;
             br = x >> 32;
         }
-        if (!br)
-            for (int i = 0; i <= N; ++i) t[i] = d[i];
+        for (int i = 0; i <= N; ++i) t[i] = br ? t[i] : d[i];
     }
     for (int i = 0; i < N; ++i) r[i] = t[i];
 }
 
 // out = 1 / y mod m (plain integers, y in [1, m), m odd, gcd(y, m) = 1).  Returns the number of
 // outer steps (<= 2 * bitlen(m) / K + 2 for valid input; capped so a bad input still ends).
+// The (u, v) update of outer step k is independent of the (a, b) work of step k + 1, so it runs
+// one step late, in the same basic block as the next inner loop (software pipelining: the lone
+// lane's dependency chains interleave instead of running back to back); the first step's pending
+// update is the identity (f, g) = (2^K, 0), (0, 2^K).
 template <int N>
 MBLS_HD int inverse(uint32_t (&out)[N], const uint32_t (&y)[N], const uint32_t (&m)[N], uint32_t ninv) {
     uint32_t a[N], b[N], u[N], v[N];
@@ -179,6 +179,7 @@ MBLS_HD int inverse(uint32_t (&out)[N], const uint32_t (&y)[N], const uint32_t (
         u[i] = i == 0 ? 1u : 0u;
         v[i] = 0;
     }
+    int64_t pf0 = (int64_t)1 << K, pg0 = 0, pf1 = 0, pg1 = (int64_t)1 << K;  // pending (u, v) update
     int steps = 0;
     const int cap = (64 * N) / K + 8;
     while (!is_zero<N>(a) && steps < cap) {
@@ -201,9 +202,13 @@ MBLS_HD int inverse(uint32_t (&out)[N], const uint32_t (&y)[N], const uint32_t (
             F0 = odd ? G0 - G1 : G0;
             F1 = G1 << 1;
         }
+        // the previous step's (u, v) update, beside this step's inner loop
+        uint32_t nu[N], nv[N];
+        lincomb_mod<N>(nu, u, v, pf0, pg0, m, ninv);
+        lincomb_mod<N>(nv, u, v, pf1, pg1, m, ninv);
         int64_t f0 = (int32_t)(uint32_t)F0, g0 = ((int64_t)F0 - f0) >> 32;
         int64_t f1 = (int32_t)(uint32_t)F1, g1 = ((int64_t)F1 - f1) >> 32;
-        uint32_t na[N], nb[N], nu[N], nv[N];
+        uint32_t na[N], nb[N];
         if (lincomb_shift<N>(na, a, b, f0, g0)) {
             f0 = -f0;
             g0 = -g0;
@@ -212,16 +217,20 @@ MBLS_HD int inverse(uint32_t (&out)[N], const uint32_t (&y)[N], const uint32_t (
             f1 = -f1;
             g1 = -g1;
         }
-        lincomb_mod<N>(nu, u, v, f0, g0, m, ninv);
-        lincomb_mod<N>(nv, u, v, f1, g1, m, ninv);
         for (int i = 0; i < N; ++i) {
             a[i] = na[i];
             b[i] = nb[i];
             u[i] = nu[i];
             v[i] = nv[i];
         }
+        pf0 = f0;
+        pg0 = g0;
+        pf1 = f1;
+        pg1 = g1;
     }
-    for (int i = 0; i < N; ++i) out[i] = v[i];
+    uint32_t nv[N];
+    lincomb_mod<N>(nv, u, v, pf1, pg1, m, ninv);  // the last step's update (only v is needed)
+    for (int i = 0; i < N; ++i) out[i] = nv[i];
     return steps;
 }
 
