@@ -30,7 +30,8 @@ cp $KS $O/headline_kernel_stats.csv
 KS2=$(find $O/trace_g2 -name "*kernel_stats.csv") && python3 tools/prof_summary.py $KS2 \
   "G2 MSM 2^20 alone: tools/stage_probe.py --group g2 --log 20 --reps 5 (+2 warmup; setup kernels included)" > $O/g2_kernel_stats.md
 cp $KS2 $O/g2_kernel_stats.csv
-python3 tools/timeline.py $(find $O/trace -name "*kernel_trace.csv") 2 > $O/headline_timeline.txt
+# the last TIMED MSM (bench.py runs steps, then max(3, steps // 2) = 5 profiled MSMs with stage events)
+python3 tools/timeline.py $(find $O/trace -name "*kernel_trace.csv") 6 > $O/headline_timeline.txt
 python3 tools/pmc_summary.py $O/pmc > $O/pmc_summary.json || exit 1
 head -30 $O/headline_kernel_stats.md
 head -16 $O/g2_kernel_stats.md
