@@ -462,11 +462,7 @@ MBLS_DEV uint64_t divmod_x(uint32_t (&t)[8]) {
 }
 
 template <bool MONT>
-__global__ __launch_bounds__(256) void k_psi_split(const uint8_t* __restrict__ scalars, uint32_t n,
-                                                   uint4* __restrict__ out, ZeroList z) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    z.run(i, gridDim.x * blockDim.x);
-    if (i >= n) return;
+MBLS_DEV void psi_split_one(const uint8_t* __restrict__ scalars, uint32_t n, uint4* __restrict__ out, uint32_t i) {
     Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
     if (MONT) s = from_mont(s);
     uint32_t t[8];
@@ -496,6 +492,15 @@ __global__ __launch_bounds__(256) void k_psi_split(const uint8_t* __restrict__ s
     }
 }
 
+template <bool MONT>
+__global__ __launch_bounds__(256) void k_psi_split(const uint8_t* __restrict__ scalars, uint32_t n,
+                                                   uint4* __restrict__ out, ZeroList z) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    z.run(i, gridDim.x * blockDim.x);
+    if (i >= n) return;
+    psi_split_one<MONT>(scalars, n, out, i);
+}
+
 // psi(x, y) = (conj(x) * CX, conj(y) * CY), CX = (0, CX1) (oracle/pyref.py PSI_CX / PSI_CY),
 // Montgomery limbs; the table holds psi^1..3(P_i) at (j-1)*n + i
 // psi^2 x-multiplier C2 = 0x1a0111ea...00000000aaac (an Fq cube root of unity), Montgomery form
@@ -508,9 +513,21 @@ __constant__ uint32_t PSI_CY0_MONT[12] = {0xa55c9ad1u, 0x3e2f585du, 0x86c18183u,
 __constant__ uint32_t PSI_CY1_MONT[12] = {0x5aa30fdau, 0x7bcfa7a2u, 0x2a927e7cu, 0xdc17dec1u, 0x6b4ebef1u, 0x2f088dd8u,
                                           0xda74d4a7u, 0xd1ca2087u, 0x96cebc1du, 0x2da25966u, 0xbbfd87d2u, 0x0e2b7eedu};
 
-__global__ __launch_bounds__(256) void k_psi_table(const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi, uint32_t n) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// Table rows staged in LDS and written out as whole lines: a lane's 96 / 192-byte row stored
+// straight from registers is 24 / 48 dword stores at a 96 / 192-byte lane stride, partial-line
+// writes that cost 1.6 GB of HBM traffic per 2^20-point psi table (2x its 0.6 GB of rows).
+// All threads of the block call it (barriers); rows = valid rows of this block.
+template <int ROW>
+MBLS_DEV void block_rows_out(uint8_t* __restrict__ dst, const uint4* __restrict__ stage, uint32_t rows) {
+    __syncthreads();
+    const uint32_t cnt = rows * (ROW / 16);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) d[k] = stage[k];
+    __syncthreads();  // the stage is reused by the next table
+}
+
+// psi(P), psi^2(P), psi^3(P) of one G2 point, Montgomery
+MBLS_DEV void psi_images(const Affine<Fq2>& p, Affine<Fq2>& q1, Affine<Fq2>& q2, Affine<Fq2>& q3) {
     Fq cx1;
     Fq2 cy;
 #pragma unroll
@@ -519,10 +536,8 @@ __global__ __launch_bounds__(256) void k_psi_table(const uint8_t* __restrict__ b
         cy.c0.v[k] = PSI_CY0_MONT[k];
         cy.c1.v[k] = PSI_CY1_MONT[k];
     }
-    const Affine<Fq2> p = load_affine<Fq2>(bases, i);
     // psi(P): conj(x) * (CX1 u) = x1 CX1 + x0 CX1 u, conj(y) * CY (5 Fq products); identity
     // (0, 0) maps to itself
-    Affine<Fq2> q1;
     q1.x.c0 = p.x.c1 * cx1;
     q1.x.c1 = p.x.c0 * cx1;
     {  // conj(y) * CY, Karatsuba in line (fq2_mul is out of line: a call frame in scratch)
@@ -530,14 +545,45 @@ __global__ __launch_bounds__(256) void k_psi_table(const uint8_t* __restrict__ b
         const Fq t0 = a0 * cy.c0, t1 = a1 * cy.c1, t2 = (a0 + a1) * (cy.c0 + cy.c1);
         q1.y = Fq2{t0 - t1, (t2 - t0) - t1};
     }
-    store_affine<Fq2>(phi, i, q1);
     // psi^2 = (x, y) -> (C2 x, -y) with C2 in Fq (oracle/pyref.py psi, checked numerically),
     // so psi^2(P) and psi^3(P) = psi^2(psi(P)) take 2 Fq products each (15 -> 9 per point)
     Fq c2;
 #pragma unroll
     for (int k = 0; k < 12; ++k) c2.v[k] = PSI2_CX_MONT[k];
-    store_affine<Fq2>(phi, (size_t)n + i, Affine<Fq2>{Fq2{p.x.c0 * c2, p.x.c1 * c2}, neg(p.y)});
-    store_affine<Fq2>(phi, 2 * (size_t)n + i, Affine<Fq2>{Fq2{q1.x.c0 * c2, q1.x.c1 * c2}, neg(q1.y)});
+    q2 = Affine<Fq2>{Fq2{p.x.c0 * c2, p.x.c1 * c2}, neg(p.y)};
+    q3 = Affine<Fq2>{Fq2{q1.x.c0 * c2, q1.x.c1 * c2}, neg(q1.y)};
+}
+
+// the block's rows of the three psi tables (table j at (j - 1) n), through one 48 KB stage
+MBLS_DEV void psi_block(const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi, uint32_t n) {
+    __shared__ uint4 stage[256 * 12];
+    const uint32_t b0 = blockIdx.x * blockDim.x, i = b0 + threadIdx.x;
+    const uint32_t rows = min(blockDim.x, n - b0);
+    Affine<Fq2> q[3];
+    if (i < n) psi_images(load_affine<Fq2>(bases, i), q[0], q[1], q[2]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        if (i < n) store_affine<Fq2>(stage, threadIdx.x, q[j]);
+        block_rows_out<192>(phi + ((size_t)j * n + b0) * 192, stage, rows);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_psi_table(const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi, uint32_t n) {
+    psi_block(bases, phi, n);
+}
+
+// G2 front in one launch (the psi counterpart of k_glv_prep): thread i splits scalar i and
+// writes psi(P_i), psi^2(P_i), psi^3(P_i) -- the table on a side stream ran beside the split and
+// digit kernels and slowed both (VALU contention) more than its own time
+template <bool MONT>
+__global__ __launch_bounds__(256) void k_psi_prep(const uint8_t* __restrict__ scalars, uint32_t n,
+                                                  uint4* __restrict__ out, ZeroList z,
+                                                  const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    z.run(i, gridDim.x * blockDim.x);
+    psi_block(bases, phi, n);  // every thread (block barriers)
+    if (i >= n) return;
+    psi_split_one<MONT>(scalars, n, out, i);
 }
 
 eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st) {
@@ -590,15 +636,20 @@ __global__ __launch_bounds__(256) void k_glv_prep(const uint8_t* __restrict__ sc
                                                   const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     z.run(i, gridDim.x * blockDim.x);
-    if (i >= n) return;
-    {
-        Affine<Fq> p = load_affine<Fq>(bases, i);
-        Fq beta;
+    {  // phi rows through a 24 KB stage, written as whole lines (block_rows_out)
+        __shared__ uint4 stage[256 * 6];
+        const uint32_t b0 = blockIdx.x * blockDim.x;
+        if (i < n) {
+            Affine<Fq> p = load_affine<Fq>(bases, i);
+            Fq beta;
 #pragma unroll
-        for (int k = 0; k < 12; ++k) beta.v[k] = GLV_BETA_MONT[k];
-        p.x = p.x * beta;
-        store_affine<Fq>(phi, i, p);
+            for (int k = 0; k < 12; ++k) beta.v[k] = GLV_BETA_MONT[k];
+            p.x = p.x * beta;
+            store_affine<Fq>(stage, threadIdx.x, p);
+        }
+        block_rows_out<96>(phi + (size_t)b0 * 96, stage, min(blockDim.x, n - b0));
     }
+    if (i >= n) return;
     Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
     if (MONT) s = from_mont(s);
     uint32_t m1[4], m2[4];
@@ -726,6 +777,13 @@ static eIcicleError digit_sources(const uint8_t* scalars, bool mont, uint32_t n,
             hipLaunchKernelGGL(k_glv_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);
         src = (const uint32_t*)dsrc;
         nidx = 2 * n;
+    } else if (P.split == 4 && phi) {  // split + psi table fused (k_psi_prep)
+        if (mont)
+            hipLaunchKernelGGL(k_psi_prep<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi);
+        else
+            hipLaunchKernelGGL(k_psi_prep<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi);
+        src = (const uint32_t*)dsrc;
+        nidx = 4 * n;
     } else if (P.split == 4) {
         if (mont)
             hipLaunchKernelGGL(k_psi_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);

@@ -139,7 +139,7 @@ struct PartSortSizes {
 };
 bool partition_sort(const MsmPlan& P);
 PartSortSizes part_sort_sizes(const MsmPlan& P);
-// bases / phi (G1 GLV only): the phi table is written by the split kernel itself (k_glv_prep)
+// bases / phi: the endomorphism table is written by the split kernel itself (k_glv_prep, k_psi_prep)
 eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* ent,
                                 uint32_t* seg_off, uint32_t* seg_cnt, uint32_t* part_tot, uint8_t* dsrc,
                                 uint32_t* zero_word, hipStream_t st, const uint8_t* bases = nullptr,
@@ -904,6 +904,15 @@ inline bool glv_prep_fused() {
     return v;
 }
 
+// G2: the psi tables inside the split kernel (k_psi_prep; MBLS_PSI_FUSED=0: side stream, A/B)
+inline bool psi_prep_fused() {
+    static const bool v = [] {
+        const char* e = getenv("MBLS_PSI_FUSED");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 // wave-layout levels of 4-input segments with at most this many segments run as trees of 4
 // waves (k_reduce_tree4; MBLS_TREE_MAX tunes, 0 disables)
 inline uint32_t tree_max_chains() {
@@ -999,8 +1008,9 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     if ((er = ctx.ensure_side(2, 1)) != MBLS_SUCCESS) return er;
     hipStream_t side = ctx.sides[0];
     hipEvent_t* ev = ctx.events.data();
-    // G1 with the partitioned sort: the phi table is written by the split kernel (k_glv_prep)
-    const bool fused_table = P.split == 2 && psort && glv_prep_fused();
+    // with the partitioned sort the endomorphism table is written by the split kernel
+    // (k_glv_prep / k_psi_prep)
+    const bool fused_table = P.split > 1 && psort && (P.split == 2 ? glv_prep_fused() : psi_prep_fused());
     if (P.split > 1 && !fused_table) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
         MBLS_TRY(hipEventRecord(ev[0], st));
         MBLS_TRY(hipStreamWaitEvent(side, ev[0], 0));

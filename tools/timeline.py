@@ -16,7 +16,7 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     which = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if any(k in r["Kernel_Name"] for k in ("k_glv_split", "k_glv_prep", "k_psi_split"))]
+    starts = [i for i, r in enumerate(rows) if any(k in r["Kernel_Name"] for k in ("k_glv_split", "k_glv_prep", "k_psi_split", "k_psi_prep"))]
     if not starts:
         print("no MSM found")
         return
