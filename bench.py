@@ -409,10 +409,19 @@ def msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_ov
         breps = max(2, args.steps // 4)
         b_ms = max_over_ranks(timed(lambda: amd.msm("g1", sb, bases, icicle=True, scalars_mont=True, batch=B,
                                                     out=rb, stream=stream, is_async=True, n=n), breps))
+        # the first and last members against single ICICLE MSMs of the same scalars
+        one = torch.zeros((1, 18), dtype=torch.int64, device=dev)
+        same = True
+        for k in (0, B - 1):
+            amd.msm("g1", sb[k * n:(k + 1) * n], bases, icicle=True, scalars_mont=True, out=one, stream=stream, n=n)
+            torch.cuda.synchronize()
+            same = same and bool(torch.equal(one[0], rb[k]))
         out["msm_batch"] = {"batch": B, "reps": breps, "ms_per_batch": round(b_ms, 3),
                             "msm_per_sec": round(world * B * 1e3 / b_ms, 3),
-                            "note": "ICICLE batch_size (core/msm.rs msm_batch_with_device_bases), members in "
-                                    "order on the caller's stream, one (x,y,1) normalisation launch for the batch"}
+                            "members_equal_single_msm": same,
+                            "note": "ICICLE batch_size (core/msm.rs msm_batch_with_device_bases); member b's front "
+                                    "(digits, sort) and tail (reduction, fold, (x,y,1)) on two side streams beside "
+                                    "the accumulations of members b - 1 / b + 1 (TailPipe, msm_core.hpp)"}
         del sb
     return out
 

@@ -1090,6 +1090,12 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __re
     }
 }
 
+// order-histogram index of (block, bin): group-major, then bin (heaviest first: the longest
+// bucket sums start first), then block inside the group; bpg = blocks of 256 buckets per group
+MBLS_DEV uint32_t order_index(uint32_t blk, uint32_t bin, uint32_t bpg) {
+    return (blk / bpg) * (ORDER_BINS * bpg) + (SMALL_MAX - bin) * bpg + blk % bpg;
+}
+
 template <bool PACK>
 __device__ __forceinline__ void part_entry(const uint32_t* __restrict__ ent, size_t o, int FB, uint32_t& fine,
                                            uint32_t& val) {
@@ -1124,8 +1130,8 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ part_tot, uint32_t tiles, int W,
                                                    int Wg, uint32_t B, int FB, uint32_t NP,
                                                    uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets,
-                                                   uint32_t* __restrict__ sorted) {
-    __shared__ uint32_t cnt[128], pre[128], span_sh;
+                                                   uint32_t* __restrict__ sorted, ChunkCountOut cc) {
+    __shared__ uint32_t cnt[128], pre[128], span_sh, chist[ORDER_BINS];
     __shared__ uint32_t ps_stage[PS_STAGE > 0 ? PS_STAGE : 1];
     const uint32_t FBN = 1u << FB;
     const uint32_t wl = blockIdx.x / NP, part = blockIdx.x % NP;
@@ -1133,6 +1139,7 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
     const uint32_t S = ((uint32_t)(W - 1 - (int)wl) / (uint32_t)Wg + 1) * tiles;
     const uint32_t team = threadIdx.x / PS_TEAM, tl = threadIdx.x % PS_TEAM, nteams = 256 / PS_TEAM;
     if (threadIdx.x < FBN) cnt[threadIdx.x] = 0;
+    if (threadIdx.x < ORDER_BINS) chist[threadIdx.x] = 0;
     __syncthreads();
     for (uint32_t s = team; s < S; s += nteams) {
         const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
@@ -1151,7 +1158,15 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
     {
         const uint32_t lim = blockIdx.x == 0 ? (uint32_t)Wg * NP : blockIdx.x;
         uint32_t a = 0;
-        for (uint32_t k = threadIdx.x; k < lim; k += blockDim.x) a += part_tot[k];
+        if (lim <= 8 * 256) {  // independent loads (the strided loop waited one latency per step)
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t k = threadIdx.x + 256 * j;
+                a += k < lim ? part_tot[k] : 0u;
+            }
+        } else {
+            for (uint32_t k = threadIdx.x; k < lim; k += blockDim.x) a += part_tot[k];
+        }
         for (int d = 32; d > 0; d >>= 1) a += __shfl_xor(a, d, 64);
         if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = a;
     }
@@ -1164,20 +1179,49 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
         const uint32_t incl = wave_incl_scan(h0 + h1), run = incl - (h0 + h1);
         if (l == 63) span_sh = incl;  // this part's entry count
         const size_t key = (size_t)wl * B + part * FBN + 2 * l;
-        if (2 * l < FBN) {
+        if (cc.nchunks) {
+            // fused k_chunk_counts (FBN == 128: the part is one 128-bucket block of the chunk-count
+            // scan): chunk counts of the L-aligned chunks, their prefix inside the block (over
+            // `counts`), the block total, the order histogram and the running maximum
+            const uint32_t o0 = base + run, o1 = o0 + h0;
+            const uint32_t c0 = h0 ? (o0 + h0 - 1) / cc.L - o0 / cc.L + 1 : 0u;
+            const uint32_t c1 = h1 ? (o1 + h1 - 1) / cc.L - o1 / cc.L + 1 : 0u;
             pre[2 * l] = run;
-            counts[key] = h0;
-            offsets[key] = base + run;
-        }
-        if (2 * l + 1 < FBN) {
             pre[2 * l + 1] = run + h0;
-            counts[key + 1] = h1;
-            offsets[key + 1] = base + run + h0;
+            offsets[key] = o0;
+            offsets[key + 1] = o1;
+            cc.nchunks[key] = c0;
+            cc.nchunks[key + 1] = c1;
+            const uint32_t cin = wave_incl_scan(c0 + c1);
+            counts[key] = cin - (c0 + c1);
+            counts[key + 1] = cin - c1;
+            if (l == 63) cc.blk_tot[key >> CHUNK_FUSED_SHIFT] = cin;
+            if (c0 <= SMALL_MAX) atomicAdd(&chist[c0], 1u);
+            if (c1 <= SMALL_MAX) atomicAdd(&chist[c1], 1u);
+            uint32_t cm = max(c0, c1);
+            for (int d = 32; d > 0; d >>= 1) cm = max(cm, (uint32_t)__shfl_xor(cm, d, 64));
+            if (l == 0 && cm > 1 && cm > __atomic_load_n(&cc.nchunks[cc.m], __ATOMIC_RELAXED))
+                atomicMax(&cc.nchunks[cc.m], cm);
+        } else {
+            if (2 * l < FBN) {
+                pre[2 * l] = run;
+                counts[key] = h0;
+                offsets[key] = base + run;
+            }
+            if (2 * l + 1 < FBN) {
+                pre[2 * l + 1] = run + h0;
+                counts[key + 1] = h1;
+                offsets[key + 1] = base + run + h0;
+            }
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 64) offsets[(size_t)Wg * B] = psum;
     __syncthreads();
     if (threadIdx.x < FBN) cnt[threadIdx.x] = 0;
+    if (cc.nchunks && threadIdx.x < ORDER_BINS && chist[threadIdx.x]) {
+        const uint32_t blk = (uint32_t)(((size_t)wl * B + part * FBN) >> 8), bpg = (cc.m + 255) / 256;
+        atomicAdd(&cc.binhist[order_index(blk, threadIdx.x, bpg)], chist[threadIdx.x]);
+    }
     __syncthreads();
     // the part's span of `sorted` is assembled in LDS and written out in order (whole lines),
     // instead of one random 4-byte store per entry; a span larger than the stage (adversarial
@@ -1206,7 +1250,8 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
 
 eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* ent,
                                 uint32_t* seg_off, uint32_t* seg_cnt, uint32_t* part_tot, uint8_t* dsrc,
-                                uint32_t* zero_word, hipStream_t st, const uint8_t* bases, uint8_t* phi) {
+                                uint32_t* zero_word, hipStream_t st, const uint8_t* bases, uint8_t* phi,
+                                uint32_t* zero2, uint32_t nzero2) {
     if (P.B > DT_MAX_B) return MBLS_INVALID_ARGUMENT;
     const PartSortSizes z = part_sort_sizes(P);
     const uint32_t* src;
@@ -1216,6 +1261,8 @@ eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, c
     zl.n[0] = (uint32_t)P.Wg * z.NP;
     zl.p[1] = zero_word;  // the chunk-count maximum (k_chunk_counts' atomicMax), HeavyTab counters
     zl.n[1] = zero_word ? 3u : 0u;
+    zl.p[2] = zero2;  // the fused chunk-count order histograms (k_part_sort atomics)
+    zl.n[2] = zero2 ? nzero2 : 0u;
     eIcicleError er = digit_sources(scalars, mont, n, P, dsrc, zl, st, src, nidx, bases, phi);
     if (er != MBLS_SUCCESS) return er;
     dim3 g(z.segments), b(DT_THREADS);
@@ -1238,19 +1285,20 @@ eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, c
     return MBLS_SUCCESS;
 }
 
+bool part_sort_fuses_chunks(const MsmPlan& P) { return part_fine_bits(P.B) == CHUNK_FUSED_SHIFT; }
+
 eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint32_t* seg_off, const uint32_t* seg_cnt,
-                              const uint32_t* part_tot, uint32_t* part_base, uint32_t* tmp, uint32_t* counts,
-                              uint32_t* offsets, uint32_t* sorted, hipStream_t st) {
+                              const uint32_t* part_tot, uint32_t* counts, uint32_t* offsets, uint32_t* sorted,
+                              const ChunkCountOut& cc, hipStream_t st) {
     const PartSortSizes z = part_sort_sizes(P);
-    (void)part_base;
-    (void)tmp;
+    if (cc.nchunks && z.FB != CHUNK_FUSED_SHIFT) return MBLS_INVALID_ARGUMENT;
     dim3 g((uint32_t)P.Wg * z.NP), b(256);
     if (z.pack)
         hipLaunchKernelGGL(k_part_sort<true>, g, b, 0, st, ent, seg_off, seg_cnt, part_tot, z.tiles, P.W, P.Wg, P.B,
-                           z.FB, z.NP, counts, offsets, sorted);
+                           z.FB, z.NP, counts, offsets, sorted, cc);
     else
         hipLaunchKernelGGL(k_part_sort<false>, g, b, 0, st, ent, seg_off, seg_cnt, part_tot, z.tiles, P.W, P.Wg, P.B,
-                           z.FB, z.NP, counts, offsets, sorted);
+                           z.FB, z.NP, counts, offsets, sorted, cc);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }
@@ -1259,11 +1307,6 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
 // accumulation thread does exactly L additions; a chunk crossing bucket boundaries yields one
 // partial ("segment") per bucket it touches.  Segments of bucket b: the aligned chunks that
 // overlap [off_b, off_b + cnt_b).  nchunks[m] receives the maximum (heavy-bucket passes).
-// order-histogram index of (block, bin): group-major, then bin (heaviest first: the longest
-// bucket sums start first), then block inside the group; bpg = blocks of 256 buckets per group
-MBLS_DEV uint32_t order_index(uint32_t blk, uint32_t bin, uint32_t bpg) {
-    return (blk / bpg) * (ORDER_BINS * bpg) + (SMALL_MAX - bin) * bpg + blk % bpg;
-}
 
 // also the first half of the chunk_off scan: cloc[b] = exclusive prefix of the chunk counts
 // inside b's block of 256 buckets, blk_tot[block] = the block's total (k_scan_small scans the
@@ -1335,8 +1378,20 @@ uint32_t order_words(uint32_t m) { return ORDER_BINS * ((m + 255) / 256); }
 MBLS_DEV void scan_wg(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t m, uint32_t* wtot) {
     const uint32_t per = (m + 1023) / 1024;
     const uint32_t b0 = min(threadIdx.x * per, m), b1 = min(b0 + per, m);
+    // up to SCAN_REG words per thread are loaded into registers by independent loads (a runtime
+    // bounded loop issued them one latency at a time: 17 words per thread at G1 2^20, ~20 us)
+    constexpr uint32_t SCAN_REG = 24;
+    uint32_t v[SCAN_REG];
     uint32_t a = 0;
-    for (uint32_t k = b0; k < b1; ++k) a += in[k];
+    if (per <= SCAN_REG) {
+#pragma unroll
+        for (uint32_t j = 0; j < SCAN_REG; ++j) {
+            v[j] = b0 + j < b1 ? in[b0 + j] : 0u;
+            a += v[j];
+        }
+    } else {
+        for (uint32_t k = b0; k < b1; ++k) a += in[k];
+    }
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t incl = a;
     for (int d = 1; d < 64; d <<= 1) {
@@ -1348,10 +1403,18 @@ MBLS_DEV void scan_wg(const uint32_t* __restrict__ in, uint32_t* __restrict__ ou
     uint32_t wbase = 0;
     for (uint32_t k = 0; k < w; ++k) wbase += wtot[k];
     uint32_t run = wbase + incl - a;
-    for (uint32_t k = b0; k < b1; ++k) {
-        const uint32_t v = in[k];
-        out[k] = run;
-        run += v;
+    if (per <= SCAN_REG) {
+#pragma unroll
+        for (uint32_t j = 0; j < SCAN_REG; ++j) {
+            if (b0 + j < b1) out[b0 + j] = run;
+            run += v[j];
+        }
+    } else {
+        for (uint32_t k = b0; k < b1; ++k) {
+            const uint32_t x = in[k];
+            out[k] = run;
+            run += x;
+        }
     }
     if (threadIdx.x == 1023) out[m] = run;
     __syncthreads();  // wtot is reused by the next scan
@@ -1368,9 +1431,9 @@ __global__ __launch_bounds__(1024) void k_scan_small(const uint32_t* __restrict_
 }
 
 eIcicleError launch_order_scan(const uint32_t* binhist, uint32_t* binbase, uint32_t m, const uint32_t* blk_tot,
-                               uint32_t* blk_pre, hipStream_t st) {
+                               uint32_t* blk_pre, uint32_t nblk, hipStream_t st) {
     hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, binhist, binbase, order_words(m), blk_tot, blk_pre,
-                       (m + 255) / 256);
+                       nblk);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }
@@ -1396,11 +1459,11 @@ eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const ui
     return MBLS_SUCCESS;
 }
 
-// chunk_off[b] = cloc[b] + blk_pre[b / 256] (the scan begun in k_chunk_counts; chunk_off[m] =
+// chunk_off[b] = cloc[b] + blk_pre[b >> cs] (the scan begun in k_chunk_counts or k_part_sort; chunk_off[m] =
 // the total); owner[segment] = bucket; first[t] = the bucket holding position L t (the start of
 // chunk t); and the bucket order of k_bucket_order (same grid: one thread per bucket)
 __global__ __launch_bounds__(256) void k_chunk_owner(const uint32_t* __restrict__ cloc, const uint32_t* __restrict__ blk_pre,
-                                                     uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ offsets,
+                                                     int cs, uint32_t* __restrict__ chunk_off, const uint32_t* __restrict__ offsets,
                                                      uint32_t m, uint32_t L, uint32_t* __restrict__ owner,
                                                      uint32_t* __restrict__ first, const uint32_t* __restrict__ nchunks,
                                                      const uint32_t* __restrict__ binbase, uint32_t* __restrict__ perm,
@@ -1410,8 +1473,8 @@ __global__ __launch_bounds__(256) void k_chunk_owner(const uint32_t* __restrict_
     __syncthreads();
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= m) return;
-    const uint32_t k0 = cloc[b] + blk_pre[b >> 8];
-    const uint32_t k1 = b + 1 < m ? cloc[b + 1] + blk_pre[(b + 1) >> 8] : blk_pre[(m + 255) >> 8];
+    const uint32_t k0 = cloc[b] + blk_pre[b >> cs];
+    const uint32_t k1 = b + 1 < m ? cloc[b + 1] + blk_pre[(b + 1) >> cs] : blk_pre[(m + (1u << cs) - 1) >> cs];
     chunk_off[b] = k0;
     if (b + 1 == m) chunk_off[m] = k1;
     for (uint32_t k = k0; k < k1; ++k) owner[k] = b;
@@ -1432,12 +1495,12 @@ __global__ __launch_bounds__(256) void k_chunk_owner(const uint32_t* __restrict_
     }
 }
 
-eIcicleError launch_chunk_owner(const uint32_t* cloc, const uint32_t* blk_pre, uint32_t* chunk_off,
+eIcicleError launch_chunk_owner(const uint32_t* cloc, const uint32_t* blk_pre, int cs, uint32_t* chunk_off,
                                 const uint32_t* offsets, uint32_t m, uint32_t L, uint32_t* owner, uint32_t* first,
                                 const uint32_t* nchunks, const uint32_t* binbase, uint32_t* perm, HeavyTab H,
                                 hipStream_t st) {
     const uint32_t nblk = (m + 255) / 256;
-    hipLaunchKernelGGL(k_chunk_owner, dim3(nblk), dim3(256), 0, st, cloc, blk_pre, chunk_off, offsets, m, L, owner,
+    hipLaunchKernelGGL(k_chunk_owner, dim3(nblk), dim3(256), 0, st, cloc, blk_pre, cs, chunk_off, offsets, m, L, owner,
                        first, nchunks, binbase, perm, H);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;

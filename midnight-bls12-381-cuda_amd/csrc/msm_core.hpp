@@ -65,10 +65,10 @@ static constexpr int ORDER_BINS = SMALL_MAX + 1;  // k_bucket_order bins: chunk 
 
 // words a kernel clears in passing (grid-stride), instead of a hipMemsetAsync fill launch
 struct ZeroList {
-    uint32_t* p[2] = {nullptr, nullptr};
-    uint32_t n[2] = {0, 0};
+    uint32_t* p[3] = {nullptr, nullptr, nullptr};
+    uint32_t n[3] = {0, 0, 0};
     MBLS_DEV void run(uint32_t gid, uint32_t stride) const {
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < 3; ++k)
             for (uint32_t i = gid; i < n[k]; i += stride) p[k][i] = 0;
     }
 };
@@ -103,8 +103,9 @@ eIcicleError scan_exclusive(const uint32_t* in, uint32_t* out, uint32_t m, uint3
 eIcicleError launch_chunk_counts(const uint32_t* counts, const uint32_t* offsets, uint32_t* nchunks, uint32_t m,
                                  uint32_t L, uint32_t* binhist, uint32_t groups, bool zeroed, uint32_t* cloc,
                                  uint32_t* blk_tot, hipStream_t st);
+// blk_tot: the chunk-count block totals (nblk of them), scanned into blk_pre
 eIcicleError launch_order_scan(const uint32_t* binhist, uint32_t* binbase, uint32_t m, const uint32_t* blk_tot,
-                               uint32_t* blk_pre, hipStream_t st);
+                               uint32_t* blk_pre, uint32_t nblk, hipStream_t st);
 uint32_t order_words(uint32_t m);
 eIcicleError launch_scatter(const uint32_t* keys, const uint32_t* vals, const uint32_t* ranks, size_t total,
                             const uint32_t* offsets, uint32_t* sorted, hipStream_t st);
@@ -120,7 +121,8 @@ struct HeavyTab {
     uint32_t* owner;    // slice g -> its entry
     uint8_t* res;       // slice g -> its sum (Jacobian)
 };
-eIcicleError launch_chunk_owner(const uint32_t* cloc, const uint32_t* blk_pre, uint32_t* chunk_off,
+// cloc / blk_pre: the chunk-count prefixes inside blocks of 2^cs buckets and the blocks' scan
+eIcicleError launch_chunk_owner(const uint32_t* cloc, const uint32_t* blk_pre, int cs, uint32_t* chunk_off,
                                 const uint32_t* offsets, uint32_t m, uint32_t L, uint32_t* owner, uint32_t* first,
                                 const uint32_t* nchunks, const uint32_t* binbase, uint32_t* perm, HeavyTab H,
                                 hipStream_t st);
@@ -140,13 +142,25 @@ struct PartSortSizes {
 bool partition_sort(const MsmPlan& P);
 PartSortSizes part_sort_sizes(const MsmPlan& P);
 // bases / phi: the endomorphism table is written by the split kernel itself (k_glv_prep, k_psi_prep)
+// chunk counts computed by the partition sort itself (k_part_sort, parts of 128 fine buckets):
+// k_chunk_counts' outputs with the prefixes in blocks of 128 buckets (CHUNK_FUSED_SHIFT)
+struct ChunkCountOut {
+    uint32_t* nchunks = nullptr;  // null: not fused (k_part_sort writes the bucket counts)
+    uint32_t* binhist = nullptr;  // order histograms (accumulated: zeroed by the digit pass)
+    uint32_t* blk_tot = nullptr;  // per 128-bucket block: the chunk-count total
+    uint32_t L = 0, m = 0;        // chunk length, bucket count
+};
+static constexpr int CHUNK_FUSED_SHIFT = 7;
+bool part_sort_fuses_chunks(const MsmPlan& P);
+// zero2 / nzero2: words the digit pass clears besides its own (the fused order histograms)
 eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* ent,
                                 uint32_t* seg_off, uint32_t* seg_cnt, uint32_t* part_tot, uint8_t* dsrc,
                                 uint32_t* zero_word, hipStream_t st, const uint8_t* bases = nullptr,
-                                uint8_t* phi = nullptr);
+                                uint8_t* phi = nullptr, uint32_t* zero2 = nullptr, uint32_t nzero2 = 0);
+// counts: the bucket counts, or with cc.nchunks the chunk-count prefixes (cloc)
 eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint32_t* seg_off, const uint32_t* seg_cnt,
-                              const uint32_t* part_tot, uint32_t* part_base, uint32_t* tmp, uint32_t* counts,
-                              uint32_t* offsets, uint32_t* sorted, hipStream_t st);
+                              const uint32_t* part_tot, uint32_t* counts, uint32_t* offsets, uint32_t* sorted,
+                              const ChunkCountOut& cc, hipStream_t st);
 
 // ------------------------------------------------------------------------------------
 // 4. accumulation: thread t sums the L contributions at sorted positions [L t, L t + L),
@@ -822,7 +836,7 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     z.perm = align_up((size_t)P.TB * 4);
     // + the chunk-count block totals and their prefixes (k_chunk_counts / k_scan_small)
     z.tmp = align_up((scan_tmp_words(std::max(std::max(max_chunks, P.TB), order_words(P.TB))) +
-                      2 * ((size_t)P.TB / 256 + 2)) *
+                      2 * ((size_t)P.TB / 128 + 2)) *
                      4);
     z.owner = align_up((size_t)max_chunks * 4);
     z.first = align_up((NC / P.chunk + 2) * 4);
@@ -913,6 +927,17 @@ inline bool psi_prep_fused() {
     return v;
 }
 
+// batch_size > 1: member b's reduction and final fold on a side stream beside member b + 1's
+// front and accumulation (TailPipe); 2: member b + 1's front on a second side stream beside member
+// b's accumulation as well; 0: every member on the caller's stream (MBLS_BATCH_PIPE)
+inline int batch_pipe() {
+    static const int v = [] {
+        const char* e = getenv("MBLS_BATCH_PIPE");
+        return e ? atoi(e) : 2;
+    }();
+    return v;
+}
+
 // wave-layout levels of 4-input segments with at most this many segments run as trees of 4
 // waves (k_reduce_tree4; MBLS_TREE_MAX tunes, 0 disables)
 inline uint32_t tree_max_chains() {
@@ -943,15 +968,35 @@ inline void launch_reduce_scaled(int mode, const uint8_t* V, const uint8_t* U, u
                            seg_log, Wl, off, Vo, Uo);
 }
 
+// Batch tail pipeline (msm_call, batch_size > 1): member b's reduction levels and final fold --
+// latency-bound chains that leave most of the GPU idle -- run on a side stream while member
+// b + 1's front and accumulation run on the caller's stream.  The tail reads only the bucket
+// sums, the level buffers and the window sums of its member's scratch region (two regions,
+// alternating), so the main stream waits for member b - 2's tail (`reuse`) only before it
+// writes that region's bucket sums again.
+// The front (digits, sort, chunk tables) of member b likewise runs on a second side stream
+// beside member b - 1's accumulation: it writes only its own region's front buffers, which member
+// b - 2's accumulation and bucket sums read (`front_wait`: that member's bucket_done, or for the
+// first two members the fork from the caller's stream).
+struct TailPipe {
+    hipStream_t side = nullptr;        // the tails run here
+    hipEvent_t bucket_done = nullptr;  // recorded on the main stream after the bucket sums
+    hipEvent_t reuse = nullptr;        // non-null: the region's previous tail; waited before the bucket sums
+    hipStream_t front = nullptr;       // non-null: the front runs here
+    hipEvent_t front_wait = nullptr;   // waited on `front` before the member's front
+    hipEvent_t front_done = nullptr;   // recorded on `front` after it; the main stream waits on it
+};
+
 // Core MSM on device operands: scalars (standard or Montgomery), bases Montgomery affine
 // (F*n entries when precomputed); result: one Jacobian Montgomery point on device, or, with
 // icicle_out, ICICLE's normalised (x, y, 1) written there by the final fold's launch.
 // Everything is enqueued on `st`; side streams of the leased context are forked from it and
-// joined back, so the caller sees one stream-ordered operation.
+// joined back, so the caller sees one stream-ordered operation -- except with `pipe`, where the
+// reduction and the final fold are left on pipe->side for the caller to join.
 template <class F>
 eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t* bases, uint32_t n,
                         const MsmPlan& P, uint8_t* result, StreamCtx& ctx, hipStream_t st,
-                        uint8_t* icicle_out = nullptr) {
+                        uint8_t* icicle_out = nullptr, const TailPipe* pipe = nullptr) {
     Arena& arena = ctx.arena;
     constexpr size_t JAC = GroupTraits<F>::JAC, AFF = GroupTraits<F>::AFF;
     constexpr uint32_t LN = LaneOf<F>::LANES;  // lanes per chain in the lane-mode kernels
@@ -1004,6 +1049,12 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
+    // the front's stream: the caller's, or the batch pipeline's front stream
+    const hipStream_t main_st = st;
+    if (pipe && pipe->front) {
+        if (pipe->front_wait) MBLS_TRY(hipStreamWaitEvent(pipe->front, pipe->front_wait, 0));
+        st = pipe->front;
+    }
     // side stream: the endomorphism table overlaps the digit / sort front (fork ev[0], join ev[1])
     if ((er = ctx.ensure_side(2, 1)) != MBLS_SUCCESS) return er;
     hipStream_t side = ctx.sides[0];
@@ -1018,11 +1069,16 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         if (er != MBLS_SUCCESS) return er;
         MBLS_TRY(hipEventRecord(ev[1], side));
     }
+    // the partition sort of 128-bucket parts also computes the chunk counts (k_chunk_counts'
+    // outputs, prefixes in 128-bucket blocks): one launch fewer
+    const bool fused_cc = psort && part_sort_fuses_chunks(P);
+    const int cs = fused_cc ? CHUNK_FUSED_SHIFT : 8;
     {
         ProfScope ps("msm.digits", st);
         if (psort) {
             er = launch_digits_part(scalars, scalars_mont, n, P, ent, seg_off, seg_cnt, part_tot, dsrc, nchunks + TB, st,
-                                    fused_table ? bases : nullptr, fused_table ? phi : nullptr);
+                                    fused_table ? bases : nullptr, fused_table ? phi : nullptr,
+                                    fused_cc ? binhist : nullptr, fused_cc ? order_words(TB) : 0u);
         } else {
             MBLS_TRY(hipMemsetAsync(counts, 0, (size_t)TB * 4, st));
             er = launch_digits(scalars, scalars_mont, n, P, keys, vals, ranks, counts, dsrc, st);
@@ -1031,26 +1087,41 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     }
     {
         ProfScope ps("msm.sort", st);
-        if (psort) {  // writes counts, offsets (incl. offsets[TB]) and sorted
-            er = launch_part_sort(P, ent, seg_off, seg_cnt, part_tot, part_base, tmp, counts, offsets, sorted, st);
+        // chunk_off = exclusive scan of the chunk counts, spread over the kernels below: block
+        // prefixes in k_chunk_counts or k_part_sort (written over `counts`, no longer needed), the
+        // block totals scanned beside the order histograms, the sum in k_chunk_owner
+        uint32_t* cloc = counts;
+        const uint32_t nblk = (TB + (1u << cs) - 1) >> cs;
+        uint32_t* blk_tot = tmp;
+        uint32_t* blk_pre = tmp + (nblk + 2);
+        if (psort) {  // writes counts (or with fused_cc the chunk counts), offsets (incl. offsets[TB]) and sorted
+            ChunkCountOut cc;
+            if (fused_cc) {
+                cc.nchunks = nchunks;
+                cc.binhist = binhist;
+                cc.blk_tot = blk_tot;
+                cc.L = P.chunk;
+                cc.m = TB;
+            }
+            er = launch_part_sort(P, ent, seg_off, seg_cnt, part_tot, counts, offsets, sorted, cc, st);
             if (er != MBLS_SUCCESS) return er;
         } else if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) {
             return er;
         }
-        // chunk_off = exclusive scan of the chunk counts, spread over the three kernels below:
-        // block prefixes in k_chunk_counts (written over `counts`, no longer needed), the block
-        // totals scanned beside the order histograms, the sum in k_chunk_owner
-        uint32_t* cloc = counts;
-        uint32_t* blk_tot = tmp;
-        uint32_t* blk_pre = tmp + (TB / 256 + 2);
-        if ((er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, 1u, psort, cloc, blk_tot, st)) !=
-            MBLS_SUCCESS)
+        if (!fused_cc &&
+            (er = launch_chunk_counts(counts, offsets, nchunks, TB, P.chunk, binhist, 1u, psort, cloc, blk_tot, st)) !=
+                MBLS_SUCCESS)
             return er;
-        if ((er = launch_order_scan(binhist, binbase, TB, blk_tot, blk_pre, st)) != MBLS_SUCCESS) return er;
+        if ((er = launch_order_scan(binhist, binbase, TB, blk_tot, blk_pre, nblk, st)) != MBLS_SUCCESS) return er;
         if (!psort && (er = launch_scatter(keys, vals, ranks, NC, offsets, sorted, st)) != MBLS_SUCCESS) return er;
-        if ((er = launch_chunk_owner(cloc, blk_pre, chunk_off, offsets, TB, P.chunk, owner, first, nchunks, binbase,
+        if ((er = launch_chunk_owner(cloc, blk_pre, cs, chunk_off, offsets, TB, P.chunk, owner, first, nchunks, binbase,
                                      perm, H, st)) != MBLS_SUCCESS)
             return er;
+    }
+    if (st != main_st) {  // join: the accumulation waits for the front
+        MBLS_TRY(hipEventRecord(pipe->front_done, st));
+        st = main_st;
+        MBLS_TRY(hipStreamWaitEvent(st, pipe->front_done, 0));
     }
     const uint32_t nsplit = P.split > 1 ? n : 0xffffffffu;
     {
@@ -1067,8 +1138,14 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         // (k_bucket_small); forked heavy passes on a side stream cost ~20 us per event wait,
         // in-line empty passes ~6 us per launch (round 3 timelines)
         const uint32_t light_blocks = (TB * LN + 255) / 256;
+        if (pipe && pipe->reuse) MBLS_TRY(hipStreamWaitEvent(st, pipe->reuse, 0));
         hipLaunchKernelGGL(k_bucket_small<F>, dim3(light_blocks + HEAVY_BLOCKS), dim3(256), 0, st, chunk_off, perm, binbase,
                            order_words(TB), partials, buckets, light_blocks, H);
+    }
+    if (pipe) {  // the tail moves to the side stream
+        MBLS_TRY(hipEventRecord(pipe->bucket_done, st));
+        MBLS_TRY(hipStreamWaitEvent(pipe->side, pipe->bucket_done, 0));
+        st = pipe->side;
     }
     {
         ProfScope ps_red("msm.reduce", st);  // the levels only (k_final has its own scope)
@@ -1147,7 +1224,8 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
                 P.c, P.W, P.Wg, P.split, P.TB, P.contributions, P.chunk, P.levels);
     uint32_t max_chunks = (uint32_t)(P.contributions / P.chunk + P.TB + 1);
     size_t scratch = msm_scratch_sizes(P, JAC, AFF, max_chunks).total();
-    er = lease.reserve(st_s + st_b + st_r + scratch + 4096);
+    const bool piped = batch > 1 && batch_pipe() > 0;
+    er = lease.reserve(st_s + st_b + st_r + scratch * (piped ? 2 : 1) + 4096);
     if (er != MBLS_SUCCESS) return er;
 
     const uint8_t* d_s = static_cast<const uint8_t*>(scalars);
@@ -1179,15 +1257,35 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
                           ? (uint8_t*)results
                           : nullptr;
     const size_t mark = A.mark();
+    // events: 2-3 bucket_done, 4-5 tail done, 6-7 front done, 8 the fork (per region where paired)
+    if (piped && (er = ctx.ensure_side(9, 3)) != MBLS_SUCCESS) return er;
+    if (piped) MBLS_TRY(hipEventRecord(ctx.events[8], st));
     for (int b = 0; b < batch; ++b) {
-        A.rewind(mark);  // scratch reused across the batch (stream-ordered)
+        // scratch reused across the batch (stream-ordered); piped: two regions, alternating
+        A.rewind(mark);
+        TailPipe pipe;
+        if (piped) {
+            if ((b & 1) && !A.take(scratch)) return MBLS_ALLOCATION_FAILED;
+            pipe.side = ctx.sides[1];
+            pipe.bucket_done = ctx.events[2 + (b & 1)];
+            pipe.reuse = b >= 2 ? ctx.events[4 + (b & 1)] : nullptr;
+            pipe.front = batch_pipe() > 1 ? ctx.sides[2] : nullptr;
+            pipe.front_wait = b >= 2 ? ctx.events[2 + (b & 1)] : ctx.events[8];
+            pipe.front_done = ctx.events[6 + (b & 1)];
+        }
         const uint8_t* sb = d_s + (size_t)b * n * 32;
         const uint8_t* bb = d_b + (shared ? 0 : (size_t)b * nbases_per * AFF);
-        er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, ctx, st, direct);
+        // piped ICICLE members are normalised inside their tails (hidden but for the last one)
+        uint8_t* icicle_b = direct ? direct : (piped && entry == MSM_ICICLE ? d_r + (size_t)b * JAC : nullptr);
+        er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, ctx, st, icicle_b,
+                           piped ? &pipe : nullptr);
         if (er != MBLS_SUCCESS) return er;
+        if (piped) MBLS_TRY(hipEventRecord(ctx.events[4 + (b & 1)], pipe.side));
     }
+    // the side stream runs the tails in member order: its last event covers them all
+    if (piped) MBLS_TRY(hipStreamWaitEvent(st, ctx.events[4 + ((batch - 1) & 1)], 0));
     if (!direct) {
-        if (entry == MSM_ICICLE) {
+        if (entry == MSM_ICICLE && !piped) {
             hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch + 63) / 64), dim3(64), 0, st, d_r, d_r, batch);
             MBLS_TRY(hipGetLastError());
         }
