@@ -11,7 +11,7 @@ cd $R || exit 1
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "batch or msm_g1_2_20 or stream" --timeout 240 --timeout-method thread \
   -p no:cacheprovider > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
 tail -1 $O/pytest.txt
-for v in 0 1 2 1 2; do
+for v in 2 3 2 3; do
   MBLS_BATCH_PIPE=$v timeout -k 10 240 python bench.py --no-cpu --no-mix --steps 10 > $O/b$v.json 2> $O/b$v.err \
     || { tail -20 $O/b$v.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('pipe', sys.argv[2], d['value'], d['msm_batch'])" $O/b$v.json $v
