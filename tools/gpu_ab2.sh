@@ -14,7 +14,7 @@ i=0
 for E in "$@"; do
   i=$((i+1))
   env $E timeout -k 10 240 python bench.py --no-cpu --no-mix --steps 10 > $O/$i.json 2> $O/$i.err || { tail -20 $O/$i.err; exit 1; }
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ntt_per_sec'], d['msm_stage_ms'], d['msm_batch']['msm_per_sec'], d['msm_batch']['members_equal_single_msm'], 'host', d['msm_host_scalars_per_sec'], d['msm_pageable_host_per_sec'])" $O/$i.json "$E"
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ntt_per_sec'], d['msm_stage_ms'], d['msm_batch']['msm_per_sec'], d['msm_batch']['members_equal_single_msm'], 'host', d['msm_host_scalars_per_sec'], d['msm_pageable_host_per_sec'], 'vec', {k: v['gb_per_s'] for k, v in d['vecops'].items() if k != 'note'})" $O/$i.json "$E"
 done
 cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
   python3 $R/bench.py --headline-only --steps 5 --warmup 1 --no-cpu > $O/trace.txt 2>&1 || exit 1
