@@ -208,6 +208,38 @@ def test_ntt_vs_oracle(amd, log_n):
     assert np.array_equal(amd.to_numpy_u64(z), xn)  # exact round trip
 
 
+@pytest.mark.parametrize("log_n", [23, 24])
+def test_ntt_past_init_tables_vs_oracle(amd, log_n):
+    """sizes above the 2^22 stage tables built at init_domain: the tables are extended on first
+    use (ntt.hip build_domain); forward against the oracle's best_fft DFT (2^23) or through the
+    inverse (2^24: exact round trip plus a forward-NTT linearity check), three 8-stage passes"""
+    import torch
+    amd.ntt_init_domain()
+    n = 1 << log_n
+    x = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(x, 0x5EED0060 + log_n, montgomery=True)
+    y = torch.zeros_like(x)
+    amd.ntt(x, inverse=False, out=y)
+    z = torch.zeros_like(x)
+    amd.ntt(y, inverse=True, out=z)
+    torch.cuda.synchronize()
+    xn = amd.to_numpy_u64(x)
+    assert np.array_equal(amd.to_numpy_u64(z), xn)  # exact round trip
+    if log_n == 23:
+        assert np.array_equal(amd.to_numpy_u64(y), H.oracle_ntt(xn, log_n, False))
+    else:
+        # NTT(x + x) == NTT(x) + NTT(x): the sum through vec add (both canonical Montgomery)
+        xx = torch.zeros_like(x)
+        amd.vec_op("add", x, x, out=xx)
+        yy = torch.zeros_like(x)
+        amd.ntt(xx, inverse=False, out=yy)
+        y2 = torch.zeros_like(x)
+        amd.vec_op("add", y, y, out=y2)
+        torch.cuda.synchronize()
+        assert torch.equal(yy, y2)
+    del x, y, z
+
+
 def test_ntt_batch_and_inplace(amd):
     import torch
     amd.ntt_init_domain()
