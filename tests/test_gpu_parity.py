@@ -504,13 +504,16 @@ def test_msm_batch(amd, gh):
     assert cases
 
 
-@pytest.mark.parametrize("group,shared", [("g1", True), ("g1", False), ("g2", True)])
-def test_msm_batch_pipelined_device(amd, gh, group, shared):
-    """batch members run on two pipeline streams (one member's tail overlaps the next one's
-    accumulation): each member equals the single-MSM result (itself pinned to the oracle),
-    device-resident operands, odd batch size, shared and per-member bases"""
+@pytest.mark.parametrize("group,shared,log_n,batch", [("g1", True, 12, 5), ("g1", False, 12, 5), ("g2", True, 12, 5),
+                                                     ("g1", True, 16, 7), ("g2", False, 14, 4)])
+def test_msm_batch_pipelined_device(amd, gh, group, shared, log_n, batch):
+    """batch members run on pipeline streams (member b's front beside member b - 1's
+    accumulation, its tail beside member b + 1's; two scratch regions reused every other member):
+    each member equals the single-MSM result (itself pinned to the oracle), device-resident
+    operands, odd and even batch sizes, shared and per-member bases, G1 at the production window
+    size (2^16: c = 16, the fused chunk counts)"""
     import torch
-    n, batch = 1 << 12, 5
+    n = 1 << log_n
     w = 12 if group == "g1" else 24
     s = torch.zeros((batch * n, 4), dtype=torch.int64, device="cuda")
     amd.gen_scalars(s, 0x5EED00B0, montgomery=True)
