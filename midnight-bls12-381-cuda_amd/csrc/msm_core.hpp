@@ -441,8 +441,8 @@ constexpr uint32_t lanes_per_chain() { return MODE == MODE_LANE ? 1u : MODE == M
 //   V'_q = 2^s sum_t V_t                           (s doublings of R)
 // so that G_w = sum_q (q V'_q + U'_q): the same form with off = 0.  One add call site (the three
 // steps of a t alternate), one doubling call site.
-template <class F, int MODE, int MINW = 1>
-__global__ __launch_bounds__(256, MINW) void k_reduce_scaled(const uint8_t* __restrict__ V, const uint8_t* __restrict__ U,
+template <class F, int MODE>
+__global__ __launch_bounds__(256) void k_reduce_scaled(const uint8_t* __restrict__ V, const uint8_t* __restrict__ U,
                                                        uint32_t m_in, uint32_t seg_log, int Wg, int off,
                                                        uint8_t* __restrict__ Vout, uint8_t* __restrict__ Uout) {
     MBLS_TAIL_PRIO();
@@ -938,16 +938,6 @@ inline int batch_pipe() {
     return v;
 }
 
-// piped batch tails: the lane-layout level built at <= 168 VGPRs (MBLS_TAIL_CAP=0: the 246-VGPR
-// build, which leaves room for only one accumulation wave beside it on a SIMD)
-inline bool tail_capped() {
-    static const bool v = [] {
-        const char* e = getenv("MBLS_TAIL_CAP");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
-
 // wave-layout levels of 4-input segments with at most this many segments run as trees of 4
 // waves (k_reduce_tree4; MBLS_TREE_MAX tunes, 0 disables)
 inline uint32_t tree_max_chains() {
@@ -961,17 +951,13 @@ inline uint32_t tree_max_chains() {
 // one reduction level over Wl windows (weights t + off; off = 1 at level 0: bucket t holds digit t + 1)
 template <class F>
 inline void launch_reduce_scaled(int mode, const uint8_t* V, const uint8_t* U, uint32_t m_in, uint32_t seg_log, int Wl,
-                                 int off, uint8_t* Vo, uint8_t* Uo, uint32_t chains, hipStream_t s,
-                                 bool beside = false) {
+                                 int off, uint8_t* Vo, uint8_t* Uo, uint32_t chains, hipStream_t s) {
     constexpr uint32_t LN = LaneOf<F>::LANES;
     if (mode == MODE_WAVE && seg_log == 2 && off == 0 && chains <= tree_max_chains()) {
         hipLaunchKernelGGL(k_reduce_tree4<F>, dim3(chains), dim3(256), 0, s, V, U, m_in, Vo, Uo);
         return;
     }
-    if (mode == MODE_LANE && beside)  // beside an accumulation: <= 168 VGPRs, one of its wave slots
-        hipLaunchKernelGGL((k_reduce_scaled<F, MODE_LANE, 3>), dim3((chains * LN + 255) / 256), dim3(256), 0, s, V, U,
-                           m_in, seg_log, Wl, off, Vo, Uo);
-    else if (mode == MODE_LANE)
+    if (mode == MODE_LANE)
         hipLaunchKernelGGL((k_reduce_scaled<F, MODE_LANE>), dim3((chains * LN + 255) / 256), dim3(256), 0, s, V, U, m_in,
                            seg_log, Wl, off, Vo, Uo);
     else if (mode == MODE_ROW)
@@ -1177,7 +1163,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             uint8_t* Vo = last ? nullptr : vb[l & 1];
             uint8_t* Uo = last ? windows : ub[l & 1];
             launch_reduce_scaled<F>(P.mode[l], V, U, m_in, P.seg_log[l], P.Wg, l == 0 ? 1 : 0, Vo, Uo,
-                                    m_out * (uint32_t)P.Wg, st, pipe && tail_capped());
+                                    m_out * (uint32_t)P.Wg, st);
             V = Vo;
             U = Uo;
         }
