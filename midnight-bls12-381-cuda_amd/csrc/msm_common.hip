@@ -1124,6 +1124,14 @@ static constexpr uint32_t PS_TEAM = MBLS_PS_TEAM;
 static constexpr uint32_t PS_STAGE = MBLS_PS_STAGE;
 static_assert(PS_STAGE * 4 + (2 * 128 + 1) * 4 <= LDS_LIMIT_BYTES, "MBLS_PS_STAGE too large for the workgroup LDS");
 
+// register-kept entries of the partition sort (k_part_sort): segments per team, entries per lane
+// and segment; MBLS_PS_KEEP=0 builds without it (A/B)
+static constexpr uint32_t PS_RS = 8, PS_RK = 6;
+#ifndef MBLS_PS_KEEP
+#define MBLS_PS_KEEP 1
+#endif
+static constexpr bool PS_KEEP = MBLS_PS_KEEP != 0;
+
 template <bool PACK>
 __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ ent, const uint32_t* __restrict__ seg_off,
                                                    const uint32_t* __restrict__ seg_cnt,
@@ -1141,14 +1149,49 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
     if (threadIdx.x < FBN) cnt[threadIdx.x] = 0;
     if (threadIdx.x < ORDER_BINS) chist[threadIdx.x] = 0;
     __syncthreads();
-    for (uint32_t s = team; s < S; s += nteams) {
-        const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
-        const uint32_t k = seg_cnt[seg * NP + part];
-        const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
-        for (uint32_t i = tl; i < k; i += PS_TEAM) {
-            uint32_t fine, val;
-            part_entry<PACK>(ent, o + i, FB, fine, val);
-            atomicAdd(&cnt[fine], 1u);
+    // a team owning <= PS_RS segments of <= PS_RK * PS_TEAM entries each (G1 2^20: 8 of ~64) keeps
+    // its lanes' packed entries in registers between the passes, so the placement pass reads no
+    // global memory (MBLS_PS_KEEP=0: both passes walk `ent`); the decision is per team
+    const uint32_t nseg = team < S ? (S - team + nteams - 1) / nteams : 0u;
+    uint32_t sk[PS_RS], so[PS_RS], e[PS_RS * PS_RK];
+    bool keep = PACK && PS_KEEP && nseg <= PS_RS;
+    if (keep) {
+#pragma unroll
+        for (uint32_t j = 0; j < PS_RS; ++j) {
+            sk[j] = so[j] = 0;
+            if (j < nseg) {
+                const uint32_t sj = team + j * nteams;
+                const uint32_t seg = (wl + (sj / tiles) * (uint32_t)Wg) * tiles + sj % tiles;
+                sk[j] = seg_cnt[seg * NP + part];
+                so[j] = seg * DT_TILE + seg_off[seg * NP + part];  // nseg <= PS_RS: few tiles, < 2^32
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < PS_RS; ++j) keep = keep && sk[j] <= PS_RK * PS_TEAM;
+    }
+    if (keep) {
+#pragma unroll
+        for (uint32_t j = 0; j < PS_RS; ++j)
+#pragma unroll
+            for (uint32_t q = 0; q < PS_RK; ++q) {
+                const uint32_t i = tl + q * PS_TEAM;
+                e[j * PS_RK + q] = i < sk[j] ? ent[so[j] + i] : 0u;
+            }
+#pragma unroll
+        for (uint32_t j = 0; j < PS_RS; ++j)
+#pragma unroll
+            for (uint32_t q = 0; q < PS_RK; ++q)
+                if (tl + q * PS_TEAM < sk[j]) atomicAdd(&cnt[FB ? e[j * PS_RK + q] >> (32 - FB) : 0u], 1u);
+    } else {
+        for (uint32_t s = team; s < S; s += nteams) {
+            const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
+            const uint32_t k = seg_cnt[seg * NP + part];
+            const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
+            for (uint32_t i = tl; i < k; i += PS_TEAM) {
+                uint32_t fine, val;
+                part_entry<PACK>(ent, o + i, FB, fine, val);
+                atomicAdd(&cnt[fine], 1u);
+            }
         }
     }
     // this part's base: the sum of the part totals before it (blockIdx = wl * NP + part, the
@@ -1228,18 +1271,33 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
     // bucket skew) takes the direct stores
     const uint32_t span = span_sh;
     const bool staged = span <= PS_STAGE;
-    for (uint32_t s = team; s < S; s += nteams) {
-        const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
-        const uint32_t k = seg_cnt[seg * NP + part];
-        const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
-        for (uint32_t i = tl; i < k; i += PS_TEAM) {
-            uint32_t fine, val;
-            part_entry<PACK>(ent, o + i, FB, fine, val);
-            const uint32_t pos = pre[fine] + atomicAdd(&cnt[fine], 1u);
-            if (staged)
-                ps_stage[pos] = val;
-            else
-                sorted[base + pos] = val;
+    auto place = [&](uint32_t fine, uint32_t val) {
+        const uint32_t pos = pre[fine] + atomicAdd(&cnt[fine], 1u);
+        if (staged)
+            ps_stage[pos] = val;
+        else
+            sorted[base + pos] = val;
+    };
+    if (keep) {
+        const uint32_t vmask = FB ? (1u << (32 - FB)) - 1 : ~0u;
+#pragma unroll
+        for (uint32_t j = 0; j < PS_RS; ++j)
+#pragma unroll
+            for (uint32_t q = 0; q < PS_RK; ++q)
+                if (tl + q * PS_TEAM < sk[j]) {
+                    const uint32_t x = e[j * PS_RK + q];
+                    place(FB ? x >> (32 - FB) : 0u, x & vmask);
+                }
+    } else {
+        for (uint32_t s = team; s < S; s += nteams) {
+            const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
+            const uint32_t k = seg_cnt[seg * NP + part];
+            const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
+            for (uint32_t i = tl; i < k; i += PS_TEAM) {
+                uint32_t fine, val;
+                part_entry<PACK>(ent, o + i, FB, fine, val);
+                place(fine, val);
+            }
         }
     }
     if (staged) {  // workgroup-uniform
