@@ -212,6 +212,21 @@ eIcicleError vec_sum_cuda(mbls_fr_t* output, const mbls_fr_t* input, int size, c
 eIcicleError bls12_381_batch_inv_cuda(mbls_fr_t* output, const mbls_fr_t* input, int size, const VecOpsConfig* config);
 
 /* ------------------------------------------------------------------------------------ */
+/* batch point-form conversions, reference point_ops.cu:759 / :844 / :924 (exported there as
+ * extern "C").  Montgomery in, Montgomery out; Jacobian projective (x = X/Z^2, y = Y/Z^3).
+ * affine_to_projective: (x, y) -> (x, y, 1), identity (0, 0) -> (0, 1, 0).
+ * projective_to_affine: Z = 0 -> (0, 0).  Input placement config->is_a_on_device, output
+ * config->is_result_on_device; a host output is synchronous.  size in 1..2^26, null pointers
+ * or other sizes give INVALID_ARGUMENT (as the reference).  Input and output must not overlap. */
+/* ------------------------------------------------------------------------------------ */
+eIcicleError bls12_381_g1_affine_to_projective(const mbls_g1_affine_t* input, int size, const VecOpsConfig* config,
+                                               mbls_g1_projective_t* output);
+eIcicleError bls12_381_g1_projective_to_affine(const mbls_g1_projective_t* input, int size, const VecOpsConfig* config,
+                                               mbls_g1_affine_t* output);
+eIcicleError bls12_381_g2_projective_to_affine(const mbls_g2_projective_t* input, int size, const VecOpsConfig* config,
+                                               mbls_g2_affine_t* output);
+
+/* ------------------------------------------------------------------------------------ */
 /* library utilities (no reference counterpart; used by the host API, tests and bench)   */
 /* ------------------------------------------------------------------------------------ */
 const char* mbls_version(void);

@@ -76,6 +76,7 @@ EXPORTED = [
     "mbls_profile_enable", "mbls_profile_reset", "mbls_profile_read",
     "mbls_release_stream", "mbls_release_scratch", "mbls_scratch_stats",
     "mbls_g1_msm_multi_device", "mbls_g2_msm_multi_device", "bls12_381_vector_sum",
+    "bls12_381_g1_affine_to_projective", "bls12_381_g1_projective_to_affine", "bls12_381_g2_projective_to_affine",
 ]
 
 _LIB = None
@@ -116,6 +117,8 @@ def lib():
         "mbls_release_stream": [P], "mbls_release_scratch": [],
         "mbls_g1_msm_multi_device": [P, P, P, i32, i32, P, P], "mbls_g2_msm_multi_device": [P, P, P, i32, i32, P, P],
         "bls12_381_vector_sum": [P, sz, P, P],
+        "bls12_381_g1_affine_to_projective": [P, i32, P, P], "bls12_381_g1_projective_to_affine": [P, i32, P, P],
+        "bls12_381_g2_projective_to_affine": [P, i32, P, P],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -232,6 +235,24 @@ def vec_op(op, a, b, out=None, stream=None, is_async=False, batch=1, columns_bat
     cfg = vec_config(is_a_on_device=_is_dev(a), is_b_on_device=_is_dev(b), is_result_on_device=_is_dev(out),
                      is_async=is_async, stream=stream, batch_size=batch, columns_batch=columns_batch)
     check(getattr(lib(), _VEC[op])(_p(a), _p(b), total // batch, ctypes.byref(cfg), _p(out)), _VEC[op])
+    return out
+
+
+# ----------------------------------------------------------------------------- point forms
+_CONV = {("g1", "to_projective"): ("bls12_381_g1_affine_to_projective", 18),
+         ("g1", "to_affine"): ("bls12_381_g1_projective_to_affine", 12),
+         ("g2", "to_affine"): ("bls12_381_g2_projective_to_affine", 24)}
+
+
+def convert_points(group, direction, pts, out=None, stream=None, is_async=False):
+    """Batch point-form conversion (reference point_ops.cu:759,844,924): `pts` is (n, k) uint64
+    (numpy host or torch device), Montgomery; returns (n, k') in the other form."""
+    name, words = _CONV[(group, direction)]
+    n = pts.shape[0]
+    if out is None:
+        out = np.zeros((n, words), dtype=np.uint64)
+    cfg = vec_config(is_a_on_device=_is_dev(pts), is_result_on_device=_is_dev(out), stream=stream, is_async=is_async)
+    check(getattr(lib(), name)(_p(pts), n, ctypes.byref(cfg), _p(out)), name)
     return out
 
 

@@ -92,10 +92,14 @@ void* Arena::take(size_t bytes) {
 
 // ---- per-device pool of scratch contexts ------------------------------------------------
 // Lease policy (CtxLease): among the free contexts of the current device take, in order,
-//   1. one whose last call was on this same stream (stream order already serialises it);
+//   1. one whose last call was on this same stream (preferred: stream order usually serialises it);
 //   2. an idle one (its `done` event complete, or never used), the largest arena first;
 //   3. a new context while the pool holds fewer than MBLS_SCRATCH_CONTEXTS (default 4);
-//   4. the least recently used one, with the caller's stream made to wait for its `done`.
+//   4. the least recently used one.
+// Whenever the picked context was used and its `done` is not known complete, the caller's stream
+// waits for `done` -- also in case 1: a handle equal to the last one may be a recycled stream (a
+// destroyed ICICLE / torch stream whose address came back) or the default stream after
+// mbls_release_stream, and a wait on an event recorded on the same queue costs HIP nothing.
 // If every context is leased by another thread and the pool is full, wait for a release.
 struct Pool {
     std::mutex mu;
@@ -129,8 +133,9 @@ CtxLease::CtxLease(hipStream_t st) : st_(st) {
         StreamCtx* lru = nullptr;
         for (auto& c : v) {
             if (c->busy) continue;
-            if (c->last == st && c->used) {
+            if (c->last_valid && c->last == st && c->used) {
                 pick = c.get();
+                wait = true;
                 break;
             }
             const bool is_idle = !c->used || hipEventQuery(c->done) == hipSuccess;
@@ -151,7 +156,7 @@ CtxLease::CtxLease(hipStream_t st) : st_(st) {
             v.push_back(std::move(c));
         } else if (lru) {
             pick = lru;
-            wait = true;
+            wait = lru->used;
         } else {
             P.cv.wait(lk);  // all leased by other threads
         }
@@ -171,23 +176,28 @@ CtxLease::CtxLease(hipStream_t st) : st_(st) {
 
 CtxLease::~CtxLease() {
     if (!ctx_) return;
-    // everything the call enqueued (side streams joined back) is ordered before `done`
+    // everything the call enqueued is ordered before `done`.  A call that forked work to the
+    // side streams joins them back before it returns; an early error return may not have, so
+    // the side streams' tails are joined here whenever the call forked (a join event each)
+    if (ctx_->forked) {
+        for (size_t i = 0; i < ctx_->sides.size() && i < ctx_->join_events.size(); ++i)
+            if (hipEventRecord(ctx_->join_events[i], ctx_->sides[i]) == hipSuccess)
+                (void)hipStreamWaitEvent(st_, ctx_->join_events[i], 0);
+        ctx_->forked = false;
+    }
     const bool rec = hipEventRecord(ctx_->done, st_) == hipSuccess;
     Pool& P = pool();
     std::lock_guard<std::mutex> g(P.mu);
     if (rec) ctx_->used = true;
     ctx_->last = st_;
+    ctx_->last_valid = true;
     ctx_->busy = false;
     P.cv.notify_one();
 }
 
-static bool side_priority() {
-    static const bool v = [] {
-        const char* e = getenv("MBLS_SIDE_PRIO");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
+#ifndef MBLS_SIDE_PRIO
+#define MBLS_SIDE_PRIO 1  // variant builds: 0 = side streams at the lowest priority
+#endif
 
 eIcicleError StreamCtx::ensure_side(size_t nevents, size_t nsides) {
     while (sides.size() < nsides) {
@@ -196,8 +206,11 @@ eIcicleError StreamCtx::ensure_side(size_t nevents, size_t nsides) {
         // behind the main stream's accumulation workgroups
         int least = 0, greatest = 0;
         MBLS_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        MBLS_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, side_priority() ? greatest : least));
+        MBLS_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, MBLS_SIDE_PRIO ? greatest : least));
         sides.push_back(s);
+        hipEvent_t j;
+        MBLS_TRY(hipEventCreateWithFlags(&j, hipEventDisableTiming));
+        join_events.push_back(j);
     }
     while (events.size() < nevents) {
         hipEvent_t e;
@@ -289,7 +302,7 @@ eIcicleError mbls_release_stream(void* stream) {
     std::lock_guard<std::mutex> g(P.mu);
     for (auto& kv : P.by_dev)
         for (auto& c : kv.second)
-            if (c->last == static_cast<hipStream_t>(stream)) c->last = nullptr;
+            if (c->last == static_cast<hipStream_t>(stream)) c->last_valid = false;
     return MBLS_SUCCESS;
 }
 

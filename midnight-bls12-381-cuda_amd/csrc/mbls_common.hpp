@@ -65,7 +65,12 @@ struct StreamCtx {
     std::vector<hipEvent_t> events;
     hipEvent_t done = nullptr;  // recorded on the caller's stream when a call's enqueue ends
     bool used = false;          // `done` has been recorded at least once
-    hipStream_t last = nullptr; // caller stream of the last call (cleared by mbls_release_stream)
+    hipStream_t last = nullptr; // caller stream of the last call
+    bool last_valid = false;    // `last` names a live stream (false after mbls_release_stream)
+    // the call forked work to `sides` (set at each fork): the lease joins them into the caller's
+    // stream before recording `done`, covering early error returns
+    bool forked = false;
+    std::vector<hipEvent_t> join_events;  // one per side stream
     bool busy = false;          // leased by a thread right now
     uint64_t stamp = 0;         // LRU order
     eIcicleError ensure_side(size_t nevents, size_t nsides = 1);

@@ -26,14 +26,13 @@ static int optimal_c(long long n) {
 
 int precompute_shift(int F) { return F > 1 ? (256 + F - 1) / F : 0; }
 
-// MBLS_C=<c> overrides the automatic window size (tuning sweeps; the caller's c wins)
-static int auto_c(long long n) {
-    static const int v = [] {
-        const char* e = getenv("MBLS_C");
-        return e ? atoi(e) : 0;
-    }();
-    return v >= 2 && v <= 20 ? v : optimal_c(n);
-}
+// -DMBLS_C=<c> (tools/ variant builds) overrides the automatic window size; the caller's
+// MSMConfig.c always wins.  No run-time environment switch: a prover's environment cannot
+// select an untested schedule.
+#ifndef MBLS_C
+#define MBLS_C 0
+#endif
+static int auto_c(long long n) { return MBLS_C >= 2 && MBLS_C <= 20 ? MBLS_C : optimal_c(n); }
 
 eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) {
     int c = cfg->c > 0 ? cfg->c : auto_c(n);
@@ -89,46 +88,41 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
 
 // Reduction levels for launches over Wl windows: level 0 has B inputs, level l divides by
 // 2^seg_log[l], the last has one output.  A level with many segments runs one per LANE, fewer
-// one per 16-lane ROW, few one per WAVE with shorter segments.  MBLS_ROW_SEG_LOG /
-// MBLS_WSEG_LOG / MBLS_LANE_MIN (tuning) override the row / wave segment lengths and the lane
-// threshold.
+// one per 16-lane ROW, few one per WAVE with shorter segments.  The -DMBLS_ROW_SEG_LOG /
+// MBLS_WSEG_LOG / MBLS_LANE_MIN ... macros (tools/ variant builds) override the row / wave segment
+// lengths and the lane threshold; the shipped values are the measured defaults below.
+#ifndef MBLS_ROW_SEG_LOG
+#define MBLS_ROW_SEG_LOG SEG_LOG
+#endif
+// G2: row segments of 8 and rows from 4096 segments (wave layout below): G2 2^20 12.69 ->
+// 12.57 ms against 16 / 8192 (G1: segments of 8 too since the 2-point tree rows, SEG_LOG)
+#ifndef MBLS_ROW_SEG_LOG_G2
+#define MBLS_ROW_SEG_LOG_G2 3
+#endif
+#ifndef MBLS_SEG0_LOG  // level 0, one segment per lane
+#define MBLS_SEG0_LOG SEG0_LOG
+#endif
+// measured (G1 2^20): 2 -> reduction 1.04 ms, 4 -> 1.12 ms once the narrow levels' tree sums are
+// batched; before that, short segments lost
+#ifndef MBLS_WSEG_LOG
+#define MBLS_WSEG_LOG 2
+#endif
+// level 0 one segment per lane only with >= lane_min chains (65536 at G1 2^20 with all 8
+// windows in one launch; a window group has fewer and its chains are latency-bound)
+#ifndef MBLS_LANE_MIN
+#define MBLS_LANE_MIN 32768u
+#endif
+// levels [0, lane_levels) may run one segment per lane
+#ifndef MBLS_LANE_LEVELS
+#define MBLS_LANE_LEVELS 1
+#endif
 eIcicleError plan_levels(MsmPlan& p, int Wl) {
-    static const int row_log = [] {
-        const char* e = getenv("MBLS_ROW_SEG_LOG");
-        int v = e ? atoi(e) : SEG_LOG;
-        return v >= 1 && v <= 6 ? v : SEG_LOG;
-    }();
-    // G2: row segments of 8 and rows from 4096 segments (wave layout below): G2 2^20 12.69 ->
-    // 12.57 ms against 16 / 8192 (G1: segments of 8 too since the 2-point tree rows, SEG_LOG)
-    static const int row_log_g2 = [] {
-        const char* e = getenv("MBLS_ROW_SEG_LOG_G2");
-        int v = e ? atoi(e) : 3;
-        return v >= 1 && v <= 6 ? v : 3;
-    }();
-    static const int seg0_log = [] {  // level 0, one segment per lane (MBLS_SEG0_LOG)
-        const char* e = getenv("MBLS_SEG0_LOG");
-        int v = e ? atoi(e) : SEG0_LOG;
-        return v >= 1 && v <= 6 ? v : SEG0_LOG;
-    }();
-    static const int wave_log = [] {
-        const char* e = getenv("MBLS_WSEG_LOG");
-        // measured (G1 2^20): 2 -> reduction 1.04 ms, 4 -> 1.12 ms once the narrow levels' tree
-        // sums are batched (msm_core.hpp k_tree_sum_jobs); before that, short segments lost
-        int v = e ? atoi(e) : 2;
-        return v >= 1 && v <= 6 ? v : 2;
-    }();
-    // level 0 one segment per lane only with >= lane_min chains (65536 at G1 2^20 with all 8
-    // windows in one launch; a window group has fewer and its chains are latency-bound)
-    static const uint32_t lane_min = [] {
-        const char* e = getenv("MBLS_LANE_MIN");
-        return e ? (uint32_t)atoi(e) : 32768u;
-    }();
-    // levels [0, lane_levels) may run one segment per lane (MBLS_LANE_LEVELS, default 1)
-    static const int lane_levels = [] {
-        const char* e = getenv("MBLS_LANE_LEVELS");
-        int v = e ? atoi(e) : 1;
-        return v >= 1 && v <= 4 ? v : 1;
-    }();
+    constexpr int row_log = MBLS_ROW_SEG_LOG, row_log_g2 = MBLS_ROW_SEG_LOG_G2, seg0_log = MBLS_SEG0_LOG,
+                  wave_log = MBLS_WSEG_LOG, lane_levels = MBLS_LANE_LEVELS;
+    constexpr uint32_t lane_min = MBLS_LANE_MIN;
+    static_assert(row_log >= 1 && row_log <= 6 && row_log_g2 >= 1 && row_log_g2 <= 6 && seg0_log >= 1 &&
+                      seg0_log <= 6 && wave_log >= 1 && wave_log <= 6 && lane_levels >= 1 && lane_levels <= 4,
+                  "reduction plan macros out of range");
     p.levels = 0;
     uint32_t m = p.B;
     while (true) {
@@ -940,13 +934,12 @@ static int part_fine_bits(uint32_t B) {
     return lb > 8 ? lb - 8 : 0;
 }
 
-bool partition_sort(const MsmPlan& P) {
-    static const bool on = [] {
-        const char* e = getenv("MBLS_PART_SORT");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return on && P.B <= DT_MAX_B;
-}
+// -DMBLS_PART_SORT=0 (variant builds) forces the tiled digits + scatter sort for every c; the
+// shipped library uses it for c > 16 only
+#ifndef MBLS_PART_SORT
+#define MBLS_PART_SORT 1
+#endif
+bool partition_sort(const MsmPlan& P) { return MBLS_PART_SORT && P.B <= DT_MAX_B; }
 
 PartSortSizes part_sort_sizes(const MsmPlan& P) {
     PartSortSizes s;
@@ -1614,6 +1607,11 @@ std::mutex& multi_device_mutex() {
     return *m;
 }
 
+MultiDevRes*& multi_device_last() {
+    static MultiDevRes* last = nullptr;
+    return last;
+}
+
 eIcicleError multi_device_res(int dev, MultiDevRes*& out) {
     static std::map<int, MultiDevRes>* tab = new std::map<int, MultiDevRes>();
     auto it = tab->find(dev);
@@ -1628,6 +1626,7 @@ eIcicleError multi_device_res(int dev, MultiDevRes*& out) {
     constexpr size_t JAC = GroupTraits<Fq2>::JAC;  // the larger point
     hipError_t e = hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking);
     for (int k = 0; k < MAX_SHARDS && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&r.ev[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&r.done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(&r.partials, MAX_SHARDS * JAC);
     if (e == hipSuccess) e = hipMalloc(&r.gather, (MAX_SHARDS + 1) * JAC);
     (void)hipSetDevice(cur);

@@ -789,22 +789,20 @@ struct MsmScratchSizes {
     }
 };
 
-// reduction levels with fewer segments than this run one segment per wave (MBLS_WAVE_MIN tunes;
+// reduction levels with fewer segments than this run one segment per wave (-DMBLS_WAVE_MIN tunes;
 // G2: MBLS_WAVE_MIN_G2).  An Fq2 row-sliced addition is three row products per Fq2 product in
 // series, so G2 switches to the wave layout (the three spread over rows) at more segments
 // (8192, with G2 row segments of 8: msm_common.hip plan_levels; 4096 measured 1.75 ms of G2
 // reduction at 2^20, 8192 and 16384 1.64 ms).
-inline uint32_t wave_min_chains(bool fq2 = false) {
-    static const uint32_t v = [] {
-        const char* e = getenv("MBLS_WAVE_MIN");
-        return e ? (uint32_t)atoi(e) : 2048u;
-    }();
-    static const uint32_t v2 = [] {
-        const char* e = getenv("MBLS_WAVE_MIN_G2");
-        return e ? (uint32_t)atoi(e) : 8192u;
-    }();
-    return fq2 ? v2 : v;
-}
+// Tuning knobs in this file are compile-time macros for tools/ variant builds (never run-time
+// environment reads: a prover's environment must not select untested kernels).
+#ifndef MBLS_WAVE_MIN
+#define MBLS_WAVE_MIN 2048u
+#endif
+#ifndef MBLS_WAVE_MIN_G2
+#define MBLS_WAVE_MIN_G2 8192u
+#endif
+inline uint32_t wave_min_chains(bool fq2 = false) { return fq2 ? MBLS_WAVE_MIN_G2 : MBLS_WAVE_MIN; }
 
 inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks) {
     MsmScratchSizes z;
@@ -858,16 +856,15 @@ inline bool debug_enabled() {
     return v;
 }
 
-// the accumulation kernel instance: G1 at <= 168 VGPRs (3 waves per SIMD, MBLS_ACC_W3=0: 1)
+// the accumulation kernel instance: G1 at <= 168 VGPRs (3 waves per SIMD; -DMBLS_ACC_W3=0: 1)
+#ifndef MBLS_ACC_W3
+#define MBLS_ACC_W3 1
+#endif
 using AccKernel = void (*)(const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, uint32_t,
                            const uint8_t*, const uint8_t*, uint32_t, uint32_t, uint8_t*);
 template <class F>
 inline AccKernel accumulate_kernel() {
-    static const int w3 = [] {
-        const char* e = getenv("MBLS_ACC_W3");
-        return e ? atoi(e) : 1;
-    }();
-    if (std::is_same<F, Fq>::value && w3) return k_accumulate<F, 3>;
+    if (std::is_same<F, Fq>::value && MBLS_ACC_W3) return k_accumulate<F, 3>;
     return k_accumulate<F, 1>;
 }
 
@@ -880,73 +877,31 @@ inline AccKernel accumulate_kernel() {
 // counter-checked: SQ_INSTS_VALU +5.2% at 86 instead of 16 at 2^20), and spreading NC over one
 // round of resident waves (MBLS_ACC_CHUNK=auto, 86 at G1 2^20) cut the bucket sums 0.61 ->
 // 0.19 ms but cost 3.25 -> 3.66 ms in the accumulation.
-// MBLS_ACC_CHUNK=<n> fixes it (A/B runs).
+// -DMBLS_ACC_CHUNK=<n> fixes it (variant builds).
+#ifndef MBLS_ACC_CHUNK
+#define MBLS_ACC_CHUNK 0
+#endif
 template <class F>
 inline uint32_t accumulate_chunk(const MsmPlan& P) {
-    static const long fixed = [] {
-        const char* e = getenv("MBLS_ACC_CHUNK");
-        if (!e) return -1L;
-        return strcmp(e, "auto") == 0 ? 0L : atol(e);
-    }();
-    if (fixed > 0) return (uint32_t)fixed;
-    if (fixed < 0) {
-        const size_t per_bucket = P.contributions / std::max<uint32_t>(P.TB, 1u);
-        return (uint32_t)std::max<size_t>(CHUNK, per_bucket / 8);
-    }
-    static const size_t resident = [] {
-        int dev = 0, cus = 0, blocks = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(accumulate_kernel<F>()),
-                                                         256, 0) != hipSuccess ||
-            cus <= 0 || blocks <= 0)
-            return (size_t)0;
-        return (size_t)cus * blocks * 256 / LaneOf<F>::LANES;  // chains resident at once
-    }();
-    if (!resident) return CHUNK;
-    const size_t L = (P.contributions + resident - 1) / resident;
-    return (uint32_t)std::max<size_t>(CHUNK, L);
-}
-
-// G1: the phi table inside the split kernel (k_glv_prep) instead of on a side stream
-// (MBLS_GLV_FUSED=0: side stream, A/B)
-inline bool glv_prep_fused() {
-    static const bool v = [] {
-        const char* e = getenv("MBLS_GLV_FUSED");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
-
-// G2: the psi tables inside the split kernel (k_psi_prep; MBLS_PSI_FUSED=0: side stream, A/B)
-inline bool psi_prep_fused() {
-    static const bool v = [] {
-        const char* e = getenv("MBLS_PSI_FUSED");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
+    if (MBLS_ACC_CHUNK > 0) return (uint32_t)MBLS_ACC_CHUNK;
+    const size_t per_bucket = P.contributions / std::max<uint32_t>(P.TB, 1u);
+    return (uint32_t)std::max<size_t>(CHUNK, per_bucket / 8);
 }
 
 // batch_size > 1: member b's reduction and final fold on a side stream beside member b + 1's
 // front and accumulation (TailPipe); 2: member b + 1's front on a second side stream beside member
-// b's accumulation as well; 0: every member on the caller's stream (MBLS_BATCH_PIPE)
-inline int batch_pipe() {
-    static const int v = [] {
-        const char* e = getenv("MBLS_BATCH_PIPE");
-        return e ? atoi(e) : 2;
-    }();
-    return v;
-}
+// b's accumulation as well; 0: every member on the caller's stream (-DMBLS_BATCH_PIPE)
+#ifndef MBLS_BATCH_PIPE
+#define MBLS_BATCH_PIPE 2
+#endif
+inline int batch_pipe() { return MBLS_BATCH_PIPE; }
 
 // wave-layout levels of 4-input segments with at most this many segments run as trees of 4
-// waves (k_reduce_tree4; MBLS_TREE_MAX tunes, 0 disables)
-inline uint32_t tree_max_chains() {
-    static const uint32_t v = [] {
-        const char* e = getenv("MBLS_TREE_MAX");
-        return e ? (uint32_t)atoi(e) : 512u;
-    }();
-    return v;
-}
+// waves (k_reduce_tree4; -DMBLS_TREE_MAX tunes, 0 disables)
+#ifndef MBLS_TREE_MAX
+#define MBLS_TREE_MAX 512u
+#endif
+inline uint32_t tree_max_chains() { return MBLS_TREE_MAX; }
 
 // one reduction level over Wl windows (weights t + off; off = 1 at level 0: bucket t holds digit t + 1)
 template <class F>
@@ -1060,9 +1015,10 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     hipStream_t side = ctx.sides[0];
     hipEvent_t* ev = ctx.events.data();
     // with the partitioned sort the endomorphism table is written by the split kernel
-    // (k_glv_prep / k_psi_prep)
-    const bool fused_table = P.split > 1 && psort && (P.split == 2 ? glv_prep_fused() : psi_prep_fused());
+    // (k_glv_prep / k_psi_prep); the tiled sort (c > 16) builds it on the side stream
+    const bool fused_table = P.split > 1 && psort;
     if (P.split > 1 && !fused_table) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
+        ctx.forked = true;
         MBLS_TRY(hipEventRecord(ev[0], st));
         MBLS_TRY(hipStreamWaitEvent(side, ev[0], 0));
         er = P.split == 2 ? launch_glv_table(bases, phi, n, side) : launch_psi_table(bases, phi, n, side);
@@ -1259,7 +1215,10 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     const size_t mark = A.mark();
     // events: 2-3 bucket_done, 4-5 tail done, 6-7 front done, 8 the fork (per region where paired)
     if (piped && (er = ctx.ensure_side(9, 3)) != MBLS_SUCCESS) return er;
-    if (piped) MBLS_TRY(hipEventRecord(ctx.events[8], st));
+    if (piped) {
+        ctx.forked = true;
+        MBLS_TRY(hipEventRecord(ctx.events[8], st));
+    }
     for (int b = 0; b < batch; ++b) {
         // scratch reused across the batch (stream-ordered); piped: two regions, alternating
         A.rewind(mark);
@@ -1312,8 +1271,12 @@ struct MultiDevRes {  // per device, created once, used under the multi-device l
     hipEvent_t ev[MAX_SHARDS] = {};
     uint8_t* partials = nullptr;  // MAX_SHARDS Jacobian partials (G2 size)
     uint8_t* gather = nullptr;    // (first device) MAX_SHARDS gathered partials + the sum
+    hipEvent_t done = nullptr;    // (first device) recorded on the call's first stream at its end
 };
 std::mutex& multi_device_mutex();
+// the first device's resources of the last call (its `done` orders the next call's reuse of the
+// partial / gather slots, whatever streams the two calls use); under the multi-device lock
+MultiDevRes*& multi_device_last();
 eIcicleError multi_device_res(int dev, MultiDevRes*& out);
 
 template <class F>
@@ -1345,6 +1308,9 @@ eIcicleError msm_multi_device(const void* scalars, const void* const* bases_per_
     // shard streams are forked from the caller's stream: the caller's earlier work on its
     // inputs (a device scalar upload, say) is ordered before every shard
     MBLS_TRY(hipSetDevice(d0));
+    // the previous call may still read or write the partial / gather slots on its own streams
+    // (is_async with a caller stream): this call's fork -- and so every shard -- waits for its end
+    if (MultiDevRes* last = multi_device_last()) MBLS_TRY(hipStreamWaitEvent(st0, last->done, 0));
     MBLS_TRY(hipEventRecord(r0->ev[MAX_SHARDS - 1], st0));
     const size_t n = (size_t)msm_size;
     for (int k = 0; k < ndev; ++k) {
@@ -1382,9 +1348,9 @@ eIcicleError msm_multi_device(const void* scalars, const void* const* bases_per_
     MBLS_TRY(hipGetLastError());
     MBLS_TRY(hipMemcpyAsync(result, sum, JAC, cfg->are_results_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
                             st0));
-    // the library's per-device resources are reused by the next call: it must not start before
-    // this one is done with them -- wait here unless the caller owns the first stream and the
-    // result is on the device (then the next call's shards order behind st0's event fork)
+    // the library's per-device resources are reused by the next call: it waits for `done`
+    MBLS_TRY(hipEventRecord(r0->done, st0));
+    multi_device_last() = r0;
     if (!cfg->is_async || !cfg->are_results_on_device || !cfg->stream) MBLS_TRY(hipStreamSynchronize(st0));
     return MBLS_SUCCESS;
 }

@@ -104,14 +104,30 @@ struct DomainTables {
     }
 };
 
+// One domain per device, as ICICLE keeps one backend state per device: init / release /
+// get_rou act on the calling thread's current device (the ICICLE active device is thread-local,
+// device_api.h:210-211), and a transform reads the tables of the device it runs on.  A device
+// whose domain was never initialised builds canonical tables on first use (order 2^32), so NTT
+// replicas on other GPUs of one process never read another device's
+// twiddle memory.
 struct Domain {
     int order_log = 32;  // 2^order_log: order of the initialised root (size bound)
     std::shared_ptr<DomainTables> tables;
 };
 
+static constexpr int MAX_DOMAIN_DEVICES = 64;
 static std::mutex g_domain_mu;
 // never destroyed: freeing device memory during runtime teardown at exit is unsafe
-static Domain& g_domain = *new Domain();
+static Domain* g_domains[MAX_DOMAIN_DEVICES];
+
+// the current device's domain (created on first use); caller holds g_domain_mu
+static Domain* current_domain(int* dev_out = nullptr) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DOMAIN_DEVICES) return nullptr;
+    if (!g_domains[dev]) g_domains[dev] = new Domain();
+    if (dev_out) *dev_out = dev;
+    return g_domains[dev];
+}
 
 __device__ __forceinline__ uint32_t bitrev(uint32_t x, int bits) {
     return bits == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - bits));
@@ -404,11 +420,11 @@ static Fr to_dev(const uint64_t* h) {
     return r;
 }
 
-// (re)build the stage tables up to 2^max_log; caller holds g_domain_mu.  A superseded table
-// stays alive while any snapshot of it does (DomainTables)
-static eIcicleError build_domain(int max_log, hipStream_t st) {
-    if (g_domain.tables && g_domain.tables->max_log >= max_log) return MBLS_SUCCESS;
-    const int order = g_domain.order_log;
+// (re)build the stage tables of `dom` (the current device's) up to 2^max_log; caller holds
+// g_domain_mu.  A superseded table stays alive while any snapshot of it does (DomainTables)
+static eIcicleError build_domain(Domain& dom, int max_log, hipStream_t st) {
+    if (dom.tables && dom.tables->max_log >= max_log) return MBLS_SUCCESS;
+    const int order = dom.order_log;
     if (max_log > order) return MBLS_INVALID_ARGUMENT;
     size_t count = ((size_t)1 << max_log) - 1;
     if (count == 0) count = 1;
@@ -425,7 +441,7 @@ static eIcicleError build_domain(int max_log, hipStream_t st) {
     MBLS_TRY(hipGetLastError());
     MBLS_TRY(hipStreamSynchronize(st));
     t->max_log = max_log;
-    g_domain.tables = std::move(t);
+    dom.tables = std::move(t);
     return MBLS_SUCCESS;
 }
 
@@ -505,18 +521,23 @@ eIcicleError ntt_init_domain(const mbls_fr_t* root, const NTTInitDomainConfig* c
     }
     if (K < 0) return MBLS_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lk(g_domain_mu);
-    g_domain.order_log = K;
+    Domain* dom = current_domain();
+    if (!dom) return MBLS_INVALID_DEVICE;
+    // the tables are canonical (independent of the root): a smaller order only bounds sizes
+    dom->order_log = K;
     // stage tables up to 2^22 now (2 x 128 MiB); larger sizes extend them on first use
-    return build_domain(K < 22 ? K : 22, st);
+    return build_domain(*dom, K < 22 ? K : 22, st);
 }
 
 eIcicleError ntt_release_domain() {
     std::shared_ptr<DomainTables> old;
     {
         std::lock_guard<std::mutex> lk(g_domain_mu);
-        old = std::move(g_domain.tables);
-        g_domain.tables.reset();
-        g_domain.order_log = 32;
+        Domain* dom = current_domain();
+        if (!dom) return MBLS_INVALID_DEVICE;
+        old = std::move(dom->tables);
+        dom->tables.reset();
+        dom->order_log = 32;
     }
     return MBLS_SUCCESS;  // `old` frees the tables here unless a transform still holds them
 }
@@ -583,15 +604,17 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
     std::shared_ptr<DomainTables> tables;  // snapshot: valid for the whole enqueue below
     {
         std::lock_guard<std::mutex> lk(g_domain_mu);
-        if (log_n > g_domain.order_log) return MBLS_INVALID_ARGUMENT;  // beyond the initialised root
-        if (!g_domain.tables || g_domain.tables->max_log < log_n) {
-            // lazily extend the stage tables (init_domain builds up to 2^22)
+        Domain* dom = current_domain();
+        if (!dom) return MBLS_INVALID_DEVICE;
+        if (log_n > dom->order_log) return MBLS_INVALID_ARGUMENT;  // beyond the initialised root
+        if (!dom->tables || dom->tables->max_log < log_n) {
+            // lazily build / extend this device's stage tables (init_domain builds up to 2^22)
             int want = log_n < 20 ? 20 : log_n;
-            if (want > g_domain.order_log) want = g_domain.order_log;
-            eIcicleError er = build_domain(want, st);
+            if (want > dom->order_log) want = dom->order_log;
+            eIcicleError er = build_domain(*dom, want, st);
             if (er != MBLS_SUCCESS) return er;
         }
-        tables = g_domain.tables;
+        tables = dom->tables;
     }
     const size_t bytes = (size_t)size * 32 * (size_t)batch;
     const size_t total = (size_t)size * batch;
@@ -696,7 +719,9 @@ eIcicleError bls12_381_field_ntt_release_domain_cuda(void) { return ntt_release_
 eIcicleError bls12_381_ntt_get_rou_from_domain(uint64_t logn, mbls_fr_t* rou) {
     if (!rou) return MBLS_INVALID_POINTER;
     std::lock_guard<std::mutex> lk(g_domain_mu);
-    if (!g_domain.tables || logn > (uint64_t)g_domain.order_log) return MBLS_INVALID_ARGUMENT;
+    Domain* dom = current_domain();
+    if (!dom) return MBLS_INVALID_DEVICE;
+    if (!dom->tables || logn > (uint64_t)dom->order_log) return MBLS_INVALID_ARGUMENT;
     canonical_omega(rou->limbs, (int)logn);
     return MBLS_SUCCESS;
 }

@@ -20,8 +20,8 @@ def shard_range(n_total: int, world: int, rank: int):
 def gather_partials(partial, world, dist, out=None):
     """all_gather one partial point per rank -> tensor [world, limbs] (same device)."""
     import torch
-    if world == 1:
-        return partial.reshape(1, -1)
+    if world == 1 and not (dist is not None and dist.is_available() and dist.is_initialized()):
+        return partial.reshape(1, -1)  # no process group: nothing to exchange
     if out is None:
         out = torch.empty((world, partial.numel()), dtype=partial.dtype, device=partial.device)
     if partial.is_cuda and dist.get_backend() != "nccl":
