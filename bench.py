@@ -11,7 +11,8 @@ standard-form result left on the device).  At N > 1 every rank runs its 2^msm_lo
 global input stream (mbls_g1_msm_jacobian), the Jacobian partials are exchanged with ONE RCCL
 all_gather over xGMI, added on the device and normalised once (the reference has
 no multi-GPU path).  value = MSMs of 2^msm_log points completed per second over all GPUs
-(weak scaling).  The other BASELINE configs are legs of the same run (see `configs` below):
+(weak scaling), from the median of the K per-step hipEvent times (the max
+over ranks), with mean / min / max and the wall-clock rate of the same K steps in `msm_step_ms`.  The other BASELINE configs are legs of the same run (see `configs` below):
 #1 vecops (GPU and the CPU path), #2 NTT 2^20 round trip, #4 the 2^24 MSM split over the N
 ranks (strong scaling, digest comparable across N), #5 G2 MSM 2^20 + 4 x NTT 2^22 on two
 streams.  Inputs are synthetic: seeded scalars and bases P_i = k_i G generated on the device.
@@ -192,14 +193,27 @@ def main():
 
     for _ in range(args.warmup):
         msm_step()
+    # per-call hipEvent times (events on the MSM's own stream, recorded
+    # between back-to-back steps: the queue never drains), `value` from their median; the K steps
+    # are also bracketed by a barrier + synchronize on both sides and wall-timed (max over ranks)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     barrier_sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record(stream)
+    for i in range(args.steps):
         msm_step()
+        evs[i + 1].record(stream)
     barrier_sync()
     msm_time = max_over_ranks(time.perf_counter() - t0)
-    ms_per_step = msm_time / args.steps * 1e3
-    msm_per_sec = world * args.steps / msm_time
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    med_ms = max_over_ranks(statistics.median(step_ms))
+    ms_per_step = med_ms
+    msm_per_sec = world * 1e3 / med_ms
+    step_stats = {"median_ms": round(med_ms, 4), "mean_ms": round(max_over_ranks(sum(step_ms) / len(step_ms)), 4),
+                  "min_ms": round(max_over_ranks(step_ms[0]), 4), "max_ms": round(max_over_ranks(step_ms[-1]), 4),
+                  "wall_ms_per_step": round(msm_time / args.steps * 1e3, 4),
+                  "wall_msm_per_sec": round(world * args.steps / msm_time, 3),
+                  "n": args.steps, "source": "hipEvents on the MSM stream, max over ranks of each statistic"}
     headline_result = result.clone()
 
     # live per-stage timing (HIP events recorded on the MSM's own stream) for the roofline
@@ -317,6 +331,7 @@ def main():
                                    f"Montgomery scalars + bases in HBM, (x,y,1) result on device); N>1: "
                                    f"sharded, RCCL all-gather of partial sums",
                        "msm_points_per_gpu": n, "ntt_size": nn, "parallelism": f"msm-shard{world}"},
+            "msm_step_ms": step_stats,
             "bit_exact": cpu.get("bit_exact") if cpu else None,
             "ntt_per_sec": round(ntt_per_sec, 3),
             "ntt_ms": round(ntt_ms, 4) if ntt_ms else None,
@@ -376,6 +391,30 @@ def msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_ov
                                                   is_async=True, n=n), reps))
     out["msm_raw_entry_per_sec"] = round(world * 1e3 / raw_ms, 3)
     del s_std
+    # prepared bases (precompute_factor 2 = the [P, phi P] table, built once per base set as the
+    # prover uploads its SRS once): the MSM's front only splits scalars
+    table = torch.zeros((2 * n, 12), dtype=torch.int64, device=dev)
+    amd.precompute_bases("g1", bases, 2, n, out=table)
+    pres = torch.zeros((1, 18), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    prep_ms = max_over_ranks(timed(lambda: amd.msm("g1", scalars, table, icicle=True, scalars_mont=True, points_mont=False,
+                                                   precompute_factor=2, out=pres, stream=stream, is_async=True, n=n),
+                                   reps))
+    amd.msm("g1", scalars, bases, icicle=True, scalars_mont=True, out=res, stream=stream, n=n)
+    torch.cuda.synchronize(dev)
+    amd.profile(True)
+    for _ in range(3):
+        amd.msm("g1", scalars, table, icicle=True, scalars_mont=True, points_mont=False, precompute_factor=2, out=pres,
+                stream=stream, is_async=True, n=n)
+    torch.cuda.synchronize(dev)
+    pprof = amd.profile_read()
+    amd.profile(False)
+    out["msm_prepared_bases"] = {"msm_per_sec": round(world * 1e3 / prep_ms, 3), "ms": round(prep_ms, 4),
+                                 "equal_to_plain": bool(torch.equal(pres, res)),
+                                 "stage_ms": {k: round(v[0] / v[1], 4) for k, v in sorted(pprof.items()) if v[1]},
+                                 "note": "precompute_factor 2 = point-major [P, phi P] table built once "
+                                         "(precompute_bases); same scalars and (x,y,1) result as `value`"}
+    del table
     # host-inclusive: scalars in pinned host memory, staged by the call (end-to-end
     # rate with the scalar H2D; never `value`)
     host_s = scalars.cpu().pin_memory()
@@ -495,6 +534,15 @@ def mix_leg(args, amd, torch, dev, rank, timed):
     g2_same, ntt_same = bool(torch.equal(res, res_iso)), bool(torch.equal(yb, yb_iso))
     assert g2_same and ntt_same, f"config #5 overlapped outputs differ from isolated: g2 {g2_same} ntt {ntt_same}"
     del yb_iso
+    # G2 with prepared bases (precompute_factor 4 = [P, psi P, psi^2 P, psi^3 P], built once)
+    table = torch.zeros((4 * n, 24), dtype=torch.int64, device=dev)
+    amd.precompute_bases("g2", bs, 4, n, out=table)
+    pres = torch.zeros_like(res)
+    torch.cuda.synchronize(dev)
+    g2p_ms = timed(lambda: amd.msm("g2", sc, table, icicle=True, scalars_mont=True, points_mont=False,
+                                   precompute_factor=4, out=pres, stream=s_a, is_async=True, n=n), reps)
+    g2p_same = bool(torch.equal(pres, res_iso))
+    del table, pres
     acc_ms = g2_stage_ms(amd, torch, dev, g2, s_a)
     i64 = pmc_counter("k_accumulate<G2>", "SQ_INSTS_VALU_INT64")
     contributions = 4 * n * ((64 + 16 - 1) // 16)  # psi split: 4n digit streams x 4 windows (c = 16)
@@ -503,6 +551,7 @@ def mix_leg(args, amd, torch, dev, rank, timed):
     issue = valu_issue_bound_ms("k_accumulate<G2>")
     return {"g2_msm_points": n, "ntt_batch": B, "ntt_size": nn, "g2_msm_ms": round(g2_ms, 3),
             "g2_msm_per_sec": round(1e3 / g2_ms, 3),
+            "g2_prepared_bases_ms": round(g2p_ms, 3), "g2_prepared_equal_to_plain": g2p_same,
             "g2_roofline_hbm_frac": round(G2_BYTES_PER_POINT * n / (g2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
             "g2_accumulate_ms": round(acc_ms, 4) if acc_ms else None,
             "g2_roofline_valu": {"kernel": "k_accumulate<G2> (pair-sliced Fq2 lanes)", "bound": "valu",

@@ -220,6 +220,18 @@ eIcicleError StreamCtx::ensure_side(size_t nevents, size_t nsides) {
     return MBLS_SUCCESS;
 }
 
+const void* pinned_host_device_pointer(const void* p) {
+    hipPointerAttribute_t a;
+    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+    // the attribute describes the allocation: offset the device alias like the host pointer
+    const char* hbase = static_cast<const char*>(a.hostPointer ? a.hostPointer : p);
+    return static_cast<const char*>(a.devicePointer) + (static_cast<const char*>(p) - hbase);
+}
+
 bool is_device_pointer(const void* p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {

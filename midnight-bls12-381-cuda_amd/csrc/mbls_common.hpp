@@ -110,6 +110,9 @@ inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 // is `p` a device (or managed) pointer?  Used only for defensive validation.
 bool is_device_pointer(const void* p);
+// device-visible alias of page-locked (pinned / registered) host memory, or nullptr for pageable
+// host memory and device memory
+const void* pinned_host_device_pointer(const void* p);
 
 // Stage profiler: when enabled (mbls_profile_enable / MBLS_PROFILE=1) a ProfScope records a
 // hipEvent pair on the stream around the enclosed launches; mbls_profile_read() sums the

@@ -46,9 +46,20 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     //   only for wide scalars: plain needs ceil((bits+1)/c) windows of n, psi 4 x ceil(64/c)).
     p.split = 1;
     p.fq2 = endo == 4;
+    p.prepared = false;
     if (endo == 2 && F == 1 && bits > 128) p.split = 2;
     if (endo == 4 && F == 1 && bits > 192 && c <= 16) p.split = 4;
     if (F > MAX_PRECOMPUTE) return MBLS_INVALID_ARGUMENT;
+    // a precomputed table of the group's endomorphism images (precompute_factor == the split:
+    // G1 2 -> [P, phi P], G2 4 -> [P, psi P, psi^2 P, psi^3 P], precompute_call) always takes the
+    // split, whatever the bit size: the per-call image table is not built (DESIGN.md "prepared
+    // bases").  c only shapes the schedule: the psi digits need c <= 16.
+    if (endo > 1 && F == endo) {
+        p.split = endo;
+        p.prepared = true;
+        F = 1;
+        if (endo == 4 && c > 16) c = 16;
+    }
     // The split halves / quarters are 128 / 64-bit digit streams.  A caller's large c (picked for
     // 255-bit scalars, e.g. MIDNIGHT_MSM_WINDOW=15) can leave the top window a few bits wide: all
     // of that window's 2^21 digits (G1 2^20) then fall into a handful of buckets -- one partition
@@ -81,6 +92,7 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     p.TB = (uint32_t)Wg * p.B;
     p.chunk = CHUNK;  // msm_call replaces it with accumulate_chunk<F>(contributions)
     p.pts = (size_t)n * (p.split > 1 ? p.split : F);  // point indices (P_i, then the images)
+    p.table = p.prepared ? p.split : F;                // bases-buffer entries per point
     p.contributions = (size_t)n * W * p.split;
     if (p.pts >= (1u << 31)) return MBLS_INVALID_ARGUMENT;
     return plan_levels(p, Wg);
@@ -361,7 +373,7 @@ template <bool MONT>
 __global__ __launch_bounds__(256) void k_digits_glv(const uint8_t* __restrict__ scalars, uint32_t n, int c, int W,
                                                     uint32_t B, uint32_t* __restrict__ keys,
                                                     uint32_t* __restrict__ vals, uint32_t* __restrict__ ranks,
-                                                    uint32_t* __restrict__ counts) {
+                                                    uint32_t* __restrict__ counts, SplitLayout lay) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
@@ -392,7 +404,7 @@ __global__ __launch_bounds__(256) void k_digits_glv(const uint8_t* __restrict__ 
                 sign ^= 1u;
                 carry = 1;
             }
-            const uint32_t idx = (uint32_t)h * n + i;
+            const uint32_t idx = lay.at(h, i);
             emit_digit(v ? (uint32_t)w * B + (v - 1) : INVALID_KEY, (idx << 1) | sign, (size_t)w * stride + idx, keys,
                        vals, ranks, counts);
         }
@@ -413,6 +425,40 @@ __global__ void k_glv_table(const uint8_t* __restrict__ bases, uint8_t* __restri
     Affine<Fq> p = load_affine<Fq>(bases, i);
     p.x = p.x * beta;
     store_affine<Fq>(phi, i, p);
+}
+
+// Host operands of an MSM (core/msm.rs:665,773 pass a HostSlice).  Page-locked host memory is
+// read by a kernel through its device alias (PCIe reads by every CU, 4 x 16 B in flight per
+// lane); hipMemcpyAsync from pinned memory ran at ~28 GB/s for the 32 MiB of a 2^20 MSM's scalars
+// (VERDICT r3), below HIP's own staged copy of PAGEABLE memory (~40 GB/s).  Pageable memory and
+// other devices' memory (multi-device shards) keep hipMemcpyAsync.
+__global__ __launch_bounds__(256) void k_copy_pinned(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+eIcicleError stage_to_device(void* dst, const void* src, size_t bytes, hipStream_t st) {
+    const void* alias = (bytes % 16 == 0 && ((uintptr_t)src & 15) == 0) ? pinned_host_device_pointer(src) : nullptr;
+    if (alias) {
+        const size_t n16 = bytes / 16;
+        size_t blocks = (n16 + 4 * 256 - 1) / (4 * 256);
+        if (blocks > 2048) blocks = 2048;
+        if (blocks == 0) return MBLS_SUCCESS;
+        hipLaunchKernelGGL(k_copy_pinned, dim3((unsigned)blocks), dim3(256), 0, st, static_cast<uint4*>(dst),
+                           static_cast<const uint4*>(alias), n16);
+        MBLS_TRY(hipGetLastError());
+        return MBLS_SUCCESS;
+    }
+    MBLS_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
+    return MBLS_SUCCESS;
 }
 
 eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st) {
@@ -456,7 +502,8 @@ MBLS_DEV uint64_t divmod_x(uint32_t (&t)[8]) {
 }
 
 template <bool MONT>
-MBLS_DEV void psi_split_one(const uint8_t* __restrict__ scalars, uint32_t n, uint4* __restrict__ out, uint32_t i) {
+MBLS_DEV void psi_split_one(const uint8_t* __restrict__ scalars, uint32_t n, uint4* __restrict__ out, uint32_t i,
+                            SplitLayout lay) {
     Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
     if (MONT) s = from_mont(s);
     uint32_t t[8];
@@ -482,17 +529,17 @@ MBLS_DEV void psi_split_one(const uint8_t* __restrict__ scalars, uint32_t n, uin
     for (int j = 0; j < 4; ++j) {
         const bool neg = (d[j] < 0) != ((j & 1) != 0);  // psi^j = [z^j] = [(-x)^j]
         const uint64_t m = (uint64_t)(d[j] < 0 ? -d[j] : d[j]);
-        out[(size_t)j * n + i] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), 0u, neg ? 0x80000000u : 0u);
+        out[lay.at(j, i)] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), 0u, neg ? 0x80000000u : 0u);
     }
 }
 
 template <bool MONT>
 __global__ __launch_bounds__(256) void k_psi_split(const uint8_t* __restrict__ scalars, uint32_t n,
-                                                   uint4* __restrict__ out, ZeroList z) {
+                                                   uint4* __restrict__ out, ZeroList z, SplitLayout lay) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     z.run(i, gridDim.x * blockDim.x);
     if (i >= n) return;
-    psi_split_one<MONT>(scalars, n, out, i);
+    psi_split_one<MONT>(scalars, n, out, i, lay);
 }
 
 // psi(x, y) = (conj(x) * CX, conj(y) * CY), CX = (0, CX1) (oracle/pyref.py PSI_CX / PSI_CY),
@@ -577,7 +624,54 @@ __global__ __launch_bounds__(256) void k_psi_prep(const uint8_t* __restrict__ sc
     z.run(i, gridDim.x * blockDim.x);
     psi_block(bases, phi, n);  // every thread (block barriers)
     if (i >= n) return;
-    psi_split_one<MONT>(scalars, n, out, i);
+    psi_split_one<MONT>(scalars, n, out, i, SplitLayout{n, 1});
+}
+
+// Prepared bases (precompute_call with precompute_factor == the split): the point-major image
+// table out[S i + j] = endo^j(P_i) -- G1 S = 2: [P, phi P]; G2 S = 4: [P, psi P, psi^2 P, psi^3 P]
+// -- built once per base set (core/msm.rs:308-332 uploads the bases once per proof), so the
+// MSM's front only splits scalars.  Rows through an LDS stage, written as whole lines.
+__global__ __launch_bounds__(256) void k_endo_table_g1(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                        uint32_t n) {
+    __shared__ uint4 stage[256 * 12];
+    const uint32_t b0 = blockIdx.x * blockDim.x, i = b0 + threadIdx.x;
+    if (i < n) {
+        Affine<Fq> p = load_affine<Fq>(in, i);
+        store_affine<Fq>(stage, 2 * threadIdx.x, p);
+        Fq beta;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) beta.v[k] = GLV_BETA_MONT[k];
+        p.x = p.x * beta;
+        store_affine<Fq>(stage, 2 * threadIdx.x + 1, p);
+    }
+    block_rows_out<192>(out + (size_t)b0 * 192, stage, min(blockDim.x, n - b0));
+}
+
+__global__ __launch_bounds__(128) void k_endo_table_g2(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                        uint32_t n) {
+    __shared__ uint4 stage[128 * 48];
+    const uint32_t b0 = blockIdx.x * blockDim.x, i = b0 + threadIdx.x;
+    if (i < n) {
+        const Affine<Fq2> p = load_affine<Fq2>(in, i);
+        Affine<Fq2> q1, q2, q3;
+        psi_images(p, q1, q2, q3);
+        store_affine<Fq2>(stage, 4 * threadIdx.x, p);
+        store_affine<Fq2>(stage, 4 * threadIdx.x + 1, q1);
+        store_affine<Fq2>(stage, 4 * threadIdx.x + 2, q2);
+        store_affine<Fq2>(stage, 4 * threadIdx.x + 3, q3);
+    }
+    block_rows_out<768>(out + (size_t)b0 * 768, stage, min(blockDim.x, n - b0));
+}
+
+eIcicleError launch_endo_table(const uint8_t* in, uint8_t* out, uint32_t n, int split, hipStream_t st) {
+    if (split == 2)
+        hipLaunchKernelGGL(k_endo_table_g1, dim3((n + 255) / 256), dim3(256), 0, st, in, out, n);
+    else if (split == 4)
+        hipLaunchKernelGGL(k_endo_table_g2, dim3((n + 127) / 128), dim3(128), 0, st, in, out, n);
+    else
+        return MBLS_INVALID_ARGUMENT;
+    MBLS_TRY(hipGetLastError());
+    return MBLS_SUCCESS;
 }
 
 eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st) {
@@ -608,7 +702,7 @@ static constexpr uint32_t DT_MAX_B = 1u << 15;
 
 template <bool MONT>
 __global__ __launch_bounds__(256) void k_glv_split(const uint8_t* __restrict__ scalars, uint32_t n,
-                                                   uint4* __restrict__ out, ZeroList z) {
+                                                   uint4* __restrict__ out, ZeroList z, SplitLayout lay) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     z.run(i, gridDim.x * blockDim.x);
     if (i >= n) return;
@@ -617,8 +711,8 @@ __global__ __launch_bounds__(256) void k_glv_split(const uint8_t* __restrict__ s
     uint32_t m1[4], m2[4];
     bool n1, n2;
     glv_split(s, m1, n1, m2, n2);
-    out[i] = make_uint4(m1[0], m1[1], m1[2], m1[3] | (n1 ? 0x80000000u : 0u));
-    out[n + i] = make_uint4(m2[0], m2[1], m2[2], m2[3] | (n2 ? 0x80000000u : 0u));
+    out[lay.at(0, i)] = make_uint4(m1[0], m1[1], m1[2], m1[3] | (n1 ? 0x80000000u : 0u));
+    out[lay.at(1, i)] = make_uint4(m2[0], m2[1], m2[2], m2[3] | (n2 ? 0x80000000u : 0u));
 }
 
 // G1 front in one launch: thread i splits scalar i (k_glv_split) AND writes phi(P_i) (k_glv_table)
@@ -757,6 +851,9 @@ static eIcicleError digit_sources(const uint8_t* scalars, bool mont, uint32_t n,
                                   const ZeroList& z, hipStream_t st, const uint32_t*& src, uint32_t& nidx,
                                   const uint8_t* bases = nullptr, uint8_t* phi = nullptr) {
     dim3 g((n + 255) / 256);
+    // digit-source (= point) index of stream j of scalar i: j n + i against the per-call image
+    // table, i S + j against a prepared point-major table [P, phi P] / [P, psi P, psi^2 P, psi^3 P]
+    const SplitLayout lay = P.prepared ? SplitLayout{1u, (uint32_t)P.split} : SplitLayout{n, 1u};
     if (P.split == 2 && phi) {  // split + phi table fused (k_glv_prep)
         if (mont)
             hipLaunchKernelGGL(k_glv_prep<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi);
@@ -766,9 +863,9 @@ static eIcicleError digit_sources(const uint8_t* scalars, bool mont, uint32_t n,
         nidx = 2 * n;
     } else if (P.split == 2) {
         if (mont)
-            hipLaunchKernelGGL(k_glv_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);
+            hipLaunchKernelGGL(k_glv_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, lay);
         else
-            hipLaunchKernelGGL(k_glv_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);
+            hipLaunchKernelGGL(k_glv_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, lay);
         src = (const uint32_t*)dsrc;
         nidx = 2 * n;
     } else if (P.split == 4 && phi) {  // split + psi table fused (k_psi_prep)
@@ -780,9 +877,9 @@ static eIcicleError digit_sources(const uint8_t* scalars, bool mont, uint32_t n,
         nidx = 4 * n;
     } else if (P.split == 4) {
         if (mont)
-            hipLaunchKernelGGL(k_psi_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);
+            hipLaunchKernelGGL(k_psi_split<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, lay);
         else
-            hipLaunchKernelGGL(k_psi_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z);
+            hipLaunchKernelGGL(k_psi_split<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, lay);
         src = (const uint32_t*)dsrc;
         nidx = 4 * n;
     } else {
@@ -818,10 +915,13 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
     }
     if (P.split == 4) return MBLS_INVALID_ARGUMENT;  // make_plan keeps psi to c <= 16
     if (P.split == 2) {
+        const SplitLayout lay = P.prepared ? SplitLayout{1u, 2u} : SplitLayout{n, 1u};
         if (mont)
-            hipLaunchKernelGGL(k_digits_glv<true>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.B, keys, vals, ranks, counts);
+            hipLaunchKernelGGL(k_digits_glv<true>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.B, keys, vals, ranks, counts,
+                               lay);
         else
-            hipLaunchKernelGGL(k_digits_glv<false>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.B, keys, vals, ranks, counts);
+            hipLaunchKernelGGL(k_digits_glv<false>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.B, keys, vals, ranks,
+                               counts, lay);
     } else if (mont)
         hipLaunchKernelGGL(k_digits<true>, g, dim3(256), 0, st, scalars, n, P.c, P.W, P.Wg, P.sF, (uint32_t)P.F, P.B, keys,
                            vals, ranks, counts);

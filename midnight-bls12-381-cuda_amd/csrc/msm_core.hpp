@@ -73,10 +73,19 @@ struct ZeroList {
     }
 };
 
+// digit-source index of stream j of point i: j * sj + i * si (blocked: sj = n, si = 1; prepared
+// point-major table: sj = 1, si = split)
+struct SplitLayout {
+    uint32_t sj, si;
+    MBLS_DEV uint32_t at(uint32_t j, uint32_t i) const { return j * sj + i * si; }
+};
+
 struct MsmPlan {
     int c, W, Wg, F;
     int sF;                     // precomputed-table block shift in bits (0: F == 1), see window_span
     int split;                  // endomorphism split: 1 none, 2 G1 GLV (phi), 4 G2 psi
+    bool prepared;              // the bases buffer is the point-major image table (no per-call table)
+    int table;                  // bases-buffer entries per point (F, or split when prepared)
     bool fq2;                   // G2 (Fq2 coordinates)
     uint32_t B, TB;
     uint32_t chunk;             // contributions per accumulation thread (accumulate_chunk)
@@ -128,7 +137,11 @@ eIcicleError launch_chunk_owner(const uint32_t* cloc, const uint32_t* blk_pre, i
                                 hipStream_t st);
 eIcicleError launch_scalars_from_mont(uint8_t* s, size_t n, hipStream_t st);
 eIcicleError launch_glv_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
+// host (pinned: a PCIe-reading copy kernel; pageable: hipMemcpyAsync) or peer memory -> device
+eIcicleError stage_to_device(void* dst, const void* src, size_t bytes, hipStream_t st);
 eIcicleError launch_psi_table(const uint8_t* bases, uint8_t* phi, uint32_t n, hipStream_t st);
+// point-major endomorphism image table (prepared bases): out[S i + j] = endo^j(P_i), S = 2 (G1) / 4 (G2)
+eIcicleError launch_endo_table(const uint8_t* in, uint8_t* out, uint32_t n, int split, hipStream_t st);
 size_t scan_tmp_words(uint32_t m);
 
 // partitioned counting sort (msm_common.hip 2b): pass A digits -> per-segment coarse parts,
@@ -806,7 +819,7 @@ inline uint32_t wave_min_chains(bool fq2 = false) { return fq2 ? MBLS_WAVE_MIN_G
 
 inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks) {
     MsmScratchSizes z;
-    z.phi = P.split > 1 ? align_up(P.pts / P.split * (P.split - 1) * aff) : 0;
+    z.phi = P.split > 1 && !P.prepared ? align_up(P.pts / P.split * (P.split - 1) * aff) : 0;
     const size_t NC = P.contributions;
     if (partition_sort(P)) {
         const PartSortSizes s = part_sort_sizes(P);
@@ -982,7 +995,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint8_t* levelT = (uint8_t*)arena.take(z.levelT);
     uint8_t* levelR = (uint8_t*)arena.take(z.levelR);
     uint8_t* windows = (uint8_t*)arena.take(z.windows);
-    uint8_t* phi = P.split > 1 ? (uint8_t*)arena.take(z.phi) : nullptr;
+    const bool img_table = P.split > 1 && !P.prepared;  // the images are built per call
+    uint8_t* phi = img_table ? (uint8_t*)arena.take(z.phi) : nullptr;
     const bool psort = partition_sort(P);
     uint32_t* ent = (uint32_t*)arena.take(z.ent);
     uint32_t* seg_off = (uint32_t*)arena.take(z.segtab);
@@ -1000,7 +1014,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     H.owner = (uint32_t*)arena.take(z.hslices);
     H.res = (uint8_t*)arena.take(z.hres);
     H.cnt = nchunks + TB + 1;
-    if (!H.res || !windows || (P.split > 1 && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
+    if (!H.res || !windows || (img_table && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
@@ -1016,8 +1030,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     hipEvent_t* ev = ctx.events.data();
     // with the partitioned sort the endomorphism table is written by the split kernel
     // (k_glv_prep / k_psi_prep); the tiled sort (c > 16) builds it on the side stream
-    const bool fused_table = P.split > 1 && psort;
-    if (P.split > 1 && !fused_table) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
+    const bool fused_table = img_table && psort;
+    if (img_table && !fused_table) {  // endomorphism images of the bases: phi(P) (G1) or psi^1..3(P) (G2)
         ctx.forked = true;
         MBLS_TRY(hipEventRecord(ev[0], st));
         MBLS_TRY(hipStreamWaitEvent(side, ev[0], 0));
@@ -1079,11 +1093,11 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         st = main_st;
         MBLS_TRY(hipStreamWaitEvent(st, pipe->front_done, 0));
     }
-    const uint32_t nsplit = P.split > 1 ? n : 0xffffffffu;
+    const uint32_t nsplit = img_table ? n : 0xffffffffu;
     {
         // the chunk count is data dependent: launch the bound, extra threads exit
         ProfScope ps("msm.accumulate", st);
-        if (P.split > 1 && !fused_table) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
+        if (img_table && !fused_table) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
         const uint32_t threads = (uint32_t)((NC + P.chunk - 1) / P.chunk) * LN;
         hipLaunchKernelGGL(accumulate_kernel<F>(), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
                            chunk_off, first, 0u, TB, bases, phi, nsplit, P.chunk, partials);
@@ -1161,10 +1175,10 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     const bool scal_mont = icicle_semantics ? cfg->are_scalars_montgomery_form : false;
     // a precomputed table (F > 1) is precompute_call output, Montgomery whatever the flag says:
     // core/msm.rs:641-643 passes are_bases_montgomery_form = !is_precomputed() = false with it
-    const bool pts_mont = icicle_semantics && P.F == 1 ? cfg->are_points_montgomery_form : true;
+    const bool pts_mont = icicle_semantics && P.table == 1 ? cfg->are_points_montgomery_form : true;
     const bool shared = cfg->are_points_shared_in_batch || batch == 1;
     const size_t n = (size_t)msm_size;
-    const size_t nbases_per = n * (size_t)P.F;
+    const size_t nbases_per = n * (size_t)P.table;
     const size_t nbases = shared ? nbases_per : nbases_per * batch;
 
     CtxLease lease(st);
@@ -1191,13 +1205,18 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
         // pageable buffer is out of the caller's memory when hipMemcpyAsync returns, a pinned one
         // is the caller's to keep alive until the stream completes (as in ICICLE)
         void* t = A.take(n * 32 * batch);
-        // hipMemcpyDefault: host memory, or another device's (mbls_g*_msm_multi_device shards)
-        MBLS_TRY(hipMemcpyAsync(t, scalars, n * 32 * batch, hipMemcpyDefault, st));
+        // pinned host memory: a copy kernel reading it over PCIe; pageable host memory or another
+        // device's (mbls_g*_msm_multi_device shards): hipMemcpyAsync (hipMemcpyDefault)
+        if ((er = stage_to_device(t, scalars, n * 32 * batch, st)) != MBLS_SUCCESS) return er;
         d_s = static_cast<const uint8_t*>(t);
     }
     if (st_b) {
         void* t = A.take(nbases * AFF);
-        MBLS_TRY(hipMemcpyAsync(t, bases, nbases * AFF, hipMemcpyDefault, st));
+        if (cfg->are_points_on_device) {
+            MBLS_TRY(hipMemcpyAsync(t, bases, nbases * AFF, hipMemcpyDefault, st));
+        } else if ((er = stage_to_device(t, bases, nbases * AFF, st)) != MBLS_SUCCESS) {
+            return er;
+        }
         if (!pts_mont) {
             hipLaunchKernelGGL(k_points_to_mont<F>, dim3((unsigned)((nbases + 255) / 256)), dim3(256), 0, st,
                                (uint8_t*)t, nbases);
@@ -1381,8 +1400,15 @@ eIcicleError precompute_call(const void* in, int n, const MSMConfig* cfg, void* 
     MBLS_TRY(hipMemcpyAsync(din, in, in_b, cfg->are_points_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
     if (!cfg->are_points_montgomery_form)
         hipLaunchKernelGGL(k_points_to_mont<F>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, din, (size_t)n);
-    hipLaunchKernelGGL(k_precompute<F>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, st, din, dout, (size_t)n, factor,
-                       precompute_shift(factor));
+    // the factor equal to the group's endomorphism split prepares the image table instead
+    // (make_plan: an MSM with that factor splits its scalars against it)
+    constexpr int endo = std::is_same<F, Fq>::value ? 2 : 4;
+    if (factor == endo) {
+        if ((er = launch_endo_table(din, dout, (uint32_t)n, endo, st)) != MBLS_SUCCESS) return er;
+    } else {
+        hipLaunchKernelGGL(k_precompute<F>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, st, din, dout, (size_t)n,
+                           factor, precompute_shift(factor));
+    }
     MBLS_TRY(hipGetLastError());
     MBLS_TRY(hipMemcpyAsync(out, dout, out_b, cfg->are_results_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
     MBLS_TRY(hipStreamSynchronize(st));

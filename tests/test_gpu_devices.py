@@ -234,3 +234,30 @@ def test_msm_multi_device_distinct_devices(amd, gh, scalars_on):
     ref = H.g1_from_affine_mont(H.oracle_msm("g1", _std_scalars(0x5EED0D51, n), amd.to_numpy_u64(b0),
                                              threads=ORACLE_THREADS))
     assert gh.decode_icicle("g1", r[0]) == ref
+
+
+@pytest.mark.parametrize("offset", [0, 3])
+def test_msm_pinned_host_operands(amd, gh, offset):
+    """host operands in page-locked memory are staged by the PCIe copy kernel (stage_to_device):
+    pinned scalars and pinned bases, also at an offset into the pinned allocation, equal to the
+    device-operand MSM and to the oracle"""
+    import torch
+    n = (1 << 15) + 9
+    s = torch.zeros((n + offset, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0D61, montgomery=True)
+    b = torch.zeros((n + offset, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 0x5EED0D62)
+    torch.cuda.synchronize()
+    s_pin = s.cpu().pin_memory()[offset:]
+    b_pin = b.cpu().pin_memory()[offset:]
+    dev_out = torch.zeros((1, 18), dtype=torch.int64, device="cuda")
+    amd.msm("g1", s[offset:], b[offset:], icicle=True, scalars_mont=True, out=dev_out)
+    r1 = amd.msm("g1", s_pin, b[offset:], icicle=True, scalars_mont=True)
+    r2 = amd.msm("g1", s_pin, b_pin, icicle=True, scalars_mont=True)
+    torch.cuda.synchronize()
+    ref_dev = amd.to_numpy_u64(dev_out)[0]
+    assert np.array_equal(np.asarray(r1)[0], ref_dev) and np.array_equal(np.asarray(r2)[0], ref_dev)
+    full = _std_scalars(0x5EED0D61, n + offset)[offset:]
+    ref = H.g1_from_affine_mont(H.oracle_msm("g1", np.ascontiguousarray(full), amd.to_numpy_u64(b)[offset:].copy(),
+                                             threads=ORACLE_THREADS))
+    assert gh.decode_icicle("g1", ref_dev) == ref
