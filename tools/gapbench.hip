@@ -1,0 +1,94 @@
+// gapbench.hip -- what delays a kernel's dispatch after its predecessor on the same stream?
+// (VERDICT r3 "What's weak 4": ~11 us idle before k_part_sort, k_accumulate, k_bucket_small,
+// k_reduce_scaled<0> and k_final_icicle, while other launches abut within 0.3 us.)
+// Each variant X is launched after a tiny kernel, 50 times; run under
+//   rocprofv3 --kernel-trace -- ./gapbench
+// and read start(X) - end(k_tiny) per variant (tools/gap_summary.py).  Variants isolate one
+// property each: VGPR count, code size, static LDS, scratch, and the combination.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+__global__ void k_tiny(unsigned* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[0] += 1;
+}
+
+// many VGPRs, little code: the clobber forces the allocation of v0..v199
+__global__ __launch_bounds__(256) void k_vgpr200(unsigned* out) {
+    asm volatile("; clobber high VGPRs" ::: "v199");
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[1] += 1;
+}
+__global__ __launch_bounds__(256) void k_vgpr96(unsigned* out) {
+    asm volatile("; clobber" ::: "v95");
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[1] += 1;
+}
+
+// large code, few VGPRs: a long straight-line integer chain every thread runs
+__global__ __launch_bounds__(256) void k_code_big(unsigned* out, unsigned a) {
+    unsigned x = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 6000; ++i) x = x * a + (unsigned)i;
+    if (x == 0x12345678u) out[2] = x;
+}
+__global__ __launch_bounds__(256) void k_code_small(unsigned* out, unsigned a) {
+    unsigned x = threadIdx.x;
+    for (int i = 0; i < 6000; ++i) x = x * a + (unsigned)i;
+    if (x == 0x12345678u) out[2] = x;
+}
+
+// 48 KiB of static LDS
+__global__ __launch_bounds__(256) void k_lds48k(unsigned* out) {
+    __shared__ unsigned s[12 * 1024];
+    for (int i = threadIdx.x; i < 12 * 1024; i += 256) s[i] = i;
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[3] += s[100];
+}
+
+// scratch: a dynamically indexed private array
+__global__ __launch_bounds__(256) void k_scratch(unsigned* out, int k) {
+    volatile unsigned a[64];
+    for (int i = 0; i < 64; ++i) a[i] = i * k;
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[4] += a[k & 63];
+}
+
+// high VGPR + big code (the shape of the gapped MSM kernels)
+__global__ __launch_bounds__(256) void k_big_both(unsigned* out, unsigned a) {
+    asm volatile("; clobber" ::: "v199");
+    unsigned x = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 6000; ++i) x = x * a + (unsigned)i;
+    if (x == 0x12345678u) out[5] = x;
+}
+
+int main() {
+    unsigned* d;
+    hipMalloc(&d, 64 * sizeof(unsigned));
+    hipMemset(d, 0, 64 * sizeof(unsigned));
+    hipStream_t st;
+    hipStreamCreate(&st);
+    const dim3 g(1024), b(256);
+    for (int rep = 0; rep < 50; ++rep) {
+        hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        hipLaunchKernelGGL(k_vgpr200, g, b, 0, st, d);
+        hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        hipLaunchKernelGGL(k_vgpr96, g, b, 0, st, d);
+        hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        hipLaunchKernelGGL(k_code_big, g, b, 0, st, d, 3u);
+        hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        hipLaunchKernelGGL(k_code_small, g, b, 0, st, d, 3u);
+        hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        hipLaunchKernelGGL(k_lds48k, g, b, 0, st, d);
+        hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        hipLaunchKernelGGL(k_scratch, g, b, 0, st, d, rep);
+        hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        hipLaunchKernelGGL(k_big_both, g, b, 0, st, d, 3u);
+        hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        // back to back: a big kernel after a big kernel
+        hipLaunchKernelGGL(k_big_both, g, b, 0, st, d, 5u);
+        hipLaunchKernelGGL(k_big_both, g, b, 0, st, d, 7u);
+    }
+    hipStreamSynchronize(st);
+    unsigned h[8];
+    hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost);
+    printf("gapbench done %u\n", h[0]);
+    return 0;
+}
