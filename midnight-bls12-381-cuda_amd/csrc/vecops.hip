@@ -79,10 +79,18 @@ __global__ __launch_bounds__(256) void k_sum_partial(uint8_t* __restrict__ out, 
 // shape: the chunk inversion is the fixed Fermat chain a^(r-2) (field.cuh:735-900; not the
 // variable-time binary GCD of inv()), and zero inputs are handled by selects, not branches.
 static constexpr int INV_CHUNK = 64;
-MBLS_DEV Fr fr_select(bool c, const Fr& a, const Fr& b) {
+// c ? a : b with a full-word mask (no data-dependent branch, whatever the compiler
+// would make of a ternary); the zero test is an OR-reduction, not an early-exit compare
+MBLS_DEV uint32_t zero_mask(const Fr& x) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= x.v[i];
+    return 0u - (uint32_t)(o == 0u);  // all ones iff x == 0
+}
+MBLS_DEV Fr fr_select(uint32_t mask, const Fr& a, const Fr& b) {
     Fr r;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+    for (int i = 0; i < 8; ++i) r.v[i] = (a.v[i] & mask) | (b.v[i] & ~mask);
     return r;
 }
 __global__ __launch_bounds__(256) void k_batch_inv(uint8_t* __restrict__ out, const uint8_t* __restrict__ in,
@@ -95,12 +103,12 @@ __global__ __launch_bounds__(256) void k_batch_inv(uint8_t* __restrict__ out, co
     for (size_t i = s; i < e; ++i) {
         const Fr x = load<FrCfg>(in + 32 * i);
         store<FrCfg>(out + 32 * i, acc);
-        acc = fr_select(x.is_zero(), acc, acc * x);
+        acc = fr_select(zero_mask(x), acc, acc * x);
     }
     Fr inv_acc = inv_fermat(acc);
     for (size_t i = e; i-- > s;) {
         const Fr x = load<FrCfg>(in + 32 * i);
-        const bool z = x.is_zero();
+        const uint32_t z = zero_mask(x);
         store<FrCfg>(out + 32 * i, fr_select(z, Fr::zero(), inv_acc * load<FrCfg>(out + 32 * i)));
         inv_acc = fr_select(z, inv_acc, inv_acc * x);
     }
