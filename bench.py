@@ -108,6 +108,9 @@ def parse():
     ap.add_argument("--mix-batch", type=int, default=4, help="NTT polynomials in the config #5 batch")
     ap.add_argument("--msm-batch", type=int, default=8, help="members of the batched-MSM leg (0: skip)")
     ap.add_argument("--headline-only", action="store_true", help="headline MSM + NTT loops only (profiling)")
+    ap.add_argument("--no-stage-profile", action="store_true",
+                    help="skip the stage-profiler passes (their hipEvent markers add ~10 us before each stage "
+                         "in a kernel trace; use for timelines)")
     return ap.parse_args()
 
 
@@ -216,13 +219,16 @@ def main():
                   "n": args.steps, "source": "hipEvents on the MSM stream, max over ranks of each statistic"}
     headline_result = result.clone()
 
-    # live per-stage timing (HIP events recorded on the MSM's own stream) for the roofline
-    amd.profile(True)
-    for _ in range(max(3, args.steps // 2)):
-        msm_step()
-    torch.cuda.synchronize(dev)
-    msm_prof = amd.profile_read()
-    amd.profile(False)
+    # live per-stage timing (HIP events recorded on the MSM's own stream) for the roofline; the
+    # timed steps above run without these events (each marker delays the next dispatch ~10 us)
+    msm_prof = {}
+    if not args.no_stage_profile:
+        amd.profile(True)
+        for _ in range(max(3, args.steps // 2)):
+            msm_step()
+        torch.cuda.synchronize(dev)
+        msm_prof = amd.profile_read()
+        amd.profile(False)
 
     extra = {}
     if not args.headline_only:
@@ -260,12 +266,14 @@ def main():
     ntt_ms_wall = max_over_ranks(timed(lambda: amd.ntt(x, out=y, stream=stream, is_async=True), args.steps,
                                        warm=args.warmup, sync_all=True))
     ntt_per_sec = world * 1e3 / ntt_ms_wall
-    amd.profile(True)
-    for _ in range(max(3, args.steps // 2)):
-        amd.ntt(x, out=y, stream=stream, is_async=True)
-    torch.cuda.synchronize(dev)
-    ntt_prof = amd.profile_read()
-    amd.profile(False)
+    ntt_prof = {}
+    if not args.no_stage_profile:
+        amd.profile(True)
+        for _ in range(max(3, args.steps // 2)):
+            amd.ntt(x, out=y, stream=stream, is_async=True)
+        torch.cuda.synchronize(dev)
+        ntt_prof = amd.profile_read()
+        amd.profile(False)
 
     legs = {}
     if not args.headline_only:
