@@ -447,6 +447,21 @@ def msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_ov
     out["msm_pageable_host_note"] = ("core/msm.rs:665-675 shape: pageable host scalars (32 MiB H2D), device bases, "
                                      "device result copied to the host; PCIe-inclusive, never `value`")
     del page_s
+    # independent MSMs on alternating streams (the reference's async shape: core/msm.rs:742 makes a
+    # stream per call): one MSM's latency-bound tail overlaps the next one's front and
+    # accumulation; each stream's calls lease their own scratch context (no false dependency)
+    s2 = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    r2 = [torch.zeros((1, 18), dtype=torch.int64, device=dev) for _ in range(2)]
+    torch.cuda.synchronize(dev)
+
+    def two_stream_pair():
+        for k in range(2):
+            amd.msm("g1", scalars, bases, icicle=True, scalars_mont=True, out=r2[k], stream=s2[k], is_async=True, n=n)
+    pair_ms = max_over_ranks(timed(two_stream_pair, max(3, args.steps // 2), warm=2))
+    out["msm_two_streams"] = {"msm_per_sec": round(world * 2e3 / pair_ms, 3), "ms_per_pair": round(pair_ms, 4),
+                              "results_equal": bool(torch.equal(r2[0], res) and torch.equal(r2[1], res)),
+                              "note": "the same 2^20 MSM issued alternately on two caller streams (async, device "
+                                      "result), as an async prover issues independent commitments; never `value`"}
     # batched MSMs (ICICLE batch_size, shared device bases): members pipelined on two streams
     if args.msm_batch > 1:
         B = args.msm_batch

@@ -13,7 +13,7 @@ O=$R/gpurun_out/prof_set
 rm -rf $O && mkdir -p $O/pmc
 cd /tmp || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
-  python3 $R/bench.py --headline-only --steps 10 --warmup 2 > $O/headline_bench.json 2> $O/headline_bench.err || exit 1
+  python3 $R/bench.py --headline-only --no-stage-profile --steps 10 --warmup 2 > $O/headline_bench.json 2> $O/headline_bench.err || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_g2 -o run --output-format csv -- \
   python3 $R/tools/stage_probe.py --group g2 --log 20 --reps 5 > $O/g2_stages.json 2> $O/g2_stages.err || exit 1
 i=0
@@ -30,8 +30,9 @@ cp $KS $O/headline_kernel_stats.csv
 KS2=$(find $O/trace_g2 -name "*kernel_stats.csv") && python3 tools/prof_summary.py $KS2 \
   "G2 MSM 2^20 alone: tools/stage_probe.py --group g2 --log 20 --reps 5 (+2 warmup; setup kernels included)" > $O/g2_kernel_stats.md
 cp $KS2 $O/g2_kernel_stats.csv
-# the last TIMED MSM (bench.py runs steps, then max(3, steps // 2) = 5 profiled MSMs with stage events)
-python3 tools/timeline.py $(find $O/trace -name "*kernel_trace.csv") 6 > $O/headline_timeline.txt
+# the last timed MSM (--no-stage-profile: no stage-profiler hipEvent markers, whose ~10 us dispatch
+# delays showed as gaps in the round-3 timeline)
+python3 tools/timeline.py $(find $O/trace -name "*kernel_trace.csv") 1 > $O/headline_timeline.txt
 python3 tools/pmc_summary.py $O/pmc > $O/pmc_summary.json || exit 1
 head -30 $O/headline_kernel_stats.md
 head -16 $O/g2_kernel_stats.md
