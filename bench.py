@@ -423,6 +423,24 @@ def msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_ov
                                  "note": "precompute_factor 2 = point-major [P, phi P] table built once "
                                          "(precompute_bases); same scalars and (x,y,1) result as `value`"}
     del table
+    # the reference's recommended MIDNIGHT_GPU_PRECOMPUTE=4 (core/config.rs:101-125) and 8: the
+    # point-major 2^(64 f) / 2^(32 f) shift tables (fewer windows: smaller tail, shorter fold)
+    pre = {}
+    for F in (4, 8):
+        tabF = torch.zeros((F * n, 12), dtype=torch.int64, device=dev)
+        amd.precompute_bases("g1", bases, F, n, out=tabF)
+        rF = torch.zeros((1, 18), dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
+        f_ms = max_over_ranks(timed(lambda: amd.msm("g1", scalars, tabF, icicle=True, scalars_mont=True,
+                                                    points_mont=False, precompute_factor=F, out=rF, stream=stream,
+                                                    is_async=True, n=n), reps))
+        pre[f"factor_{F}"] = {"msm_per_sec": round(world * 1e3 / f_ms, 3), "ms": round(f_ms, 4),
+                              "equal_to_plain": bool(torch.equal(rF, res)),
+                              "table_bytes": F * n * 96}
+        del tabF
+    out["msm_precompute_tables"] = dict(pre, note="precompute_bases once (core/msm.rs:401-506 with "
+                                        "MIDNIGHT_GPU_PRECOMPUTE=F), then MSMs of the same scalars; never `value` "
+                                        "(the reference's benchmark uploads plain bases)")
     # host-inclusive: scalars in pinned host memory, staged by the call (end-to-end
     # rate with the scalar H2D; never `value`)
     host_s = scalars.cpu().pin_memory()
