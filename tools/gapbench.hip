@@ -5,11 +5,28 @@
 //   rocprofv3 --kernel-trace -- ./gapbench
 // and read start(X) - end(k_tiny) per variant (tools/gap_summary.py).  Variants isolate one
 // property each: VGPR count, code size, static LDS, scratch, and the combination.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
 __global__ void k_tiny(unsigned* out) {
     if (threadIdx.x == 0 && blockIdx.x == 0) out[0] += 1;
+}
+// the same body under other names, to tell the event sequences apart in the trace
+__global__ void k_after_record(unsigned* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[6] += 1;
+}
+__global__ void k_after_wait_same(unsigned* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[6] += 1;
+}
+__global__ void k_after_ext_stop(unsigned* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[6] += 1;
+}
+__global__ void k_ext_launched(unsigned* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[7] += 1;
+}
+__global__ void k_after_record_timing(unsigned* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[6] += 1;
 }
 
 // many VGPRs, little code: the clobber forces the allocation of v0..v199
@@ -66,6 +83,9 @@ int main() {
     hipStream_t st;
     hipStreamCreate(&st);
     const dim3 g(1024), b(256);
+    hipEvent_t ev, evt;
+    hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    hipEventCreate(&evt);
     for (int rep = 0; rep < 50; ++rep) {
         hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
         hipLaunchKernelGGL(k_vgpr200, g, b, 0, st, d);
@@ -82,6 +102,20 @@ int main() {
         hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
         hipLaunchKernelGGL(k_big_both, g, b, 0, st, d, 3u);
         hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        // event markers: hipEventRecord (no timing / timing), a same-stream wait, and an event
+        // attached to the previous kernel by hipExtLaunchKernelGGL (no separate marker)
+        hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        hipEventRecord(ev, st);
+        hipLaunchKernelGGL(k_after_record, g, b, 0, st, d);
+        hipEventRecord(evt, st);
+        hipLaunchKernelGGL(k_after_record_timing, g, b, 0, st, d);
+        hipEventRecord(ev, st);
+        hipStreamWaitEvent(st, ev, 0);
+        hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
+        hipStreamWaitEvent(st, ev, 0);
+        hipLaunchKernelGGL(k_after_wait_same, g, b, 0, st, d);
+        hipExtLaunchKernelGGL(k_ext_launched, g, b, 0, st, nullptr, ev, 0, d);
+        hipLaunchKernelGGL(k_after_ext_stop, g, b, 0, st, d);
         // back to back: a big kernel after a big kernel
         hipLaunchKernelGGL(k_big_both, g, b, 0, st, d, 5u);
         hipLaunchKernelGGL(k_big_both, g, b, 0, st, d, 7u);
