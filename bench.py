@@ -434,9 +434,17 @@ def msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_ov
         f_ms = max_over_ranks(timed(lambda: amd.msm("g1", scalars, tabF, icicle=True, scalars_mont=True,
                                                     points_mont=False, precompute_factor=F, out=rF, stream=stream,
                                                     is_async=True, n=n), reps))
+        amd.profile(True)
+        for _ in range(3):
+            amd.msm("g1", scalars, tabF, icicle=True, scalars_mont=True, points_mont=False, precompute_factor=F,
+                    out=rF, stream=stream, is_async=True, n=n)
+        torch.cuda.synchronize(dev)
+        fprof = amd.profile_read()
+        amd.profile(False)
         pre[f"factor_{F}"] = {"msm_per_sec": round(world * 1e3 / f_ms, 3), "ms": round(f_ms, 4),
                               "equal_to_plain": bool(torch.equal(rF, res)),
-                              "table_bytes": F * n * 96}
+                              "table_bytes": F * n * 96,
+                              "stage_ms": {k: round(v[0] / v[1], 4) for k, v in sorted(fprof.items()) if v[1]}}
         del tabF
     out["msm_precompute_tables"] = dict(pre, note="precompute_bases once (core/msm.rs:401-506 with "
                                         "MIDNIGHT_GPU_PRECOMPUTE=F), then MSMs of the same scalars; never `value` "

@@ -445,8 +445,13 @@ __global__ __launch_bounds__(256) void k_copy_pinned(uint4* __restrict__ dst, co
     for (; i < n16; i += stride) dst[i] = src[i];
 }
 
+#ifndef MBLS_PINNED_KERNEL
+#define MBLS_PINNED_KERNEL 1  // variant builds: 0 = hipMemcpyAsync for pinned memory too
+#endif
 eIcicleError stage_to_device(void* dst, const void* src, size_t bytes, hipStream_t st) {
-    const void* alias = (bytes % 16 == 0 && ((uintptr_t)src & 15) == 0) ? pinned_host_device_pointer(src) : nullptr;
+    const void* alias = (MBLS_PINNED_KERNEL && bytes % 16 == 0 && ((uintptr_t)src & 15) == 0)
+                            ? pinned_host_device_pointer(src)
+                            : nullptr;
     if (alias) {
         const size_t n16 = bytes / 16;
         size_t blocks = (n16 + 4 * 256 - 1) / (4 * 256);

@@ -1159,6 +1159,9 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
 // sharded multi-GPU MSM: partials are summed before the one normalisation)
 enum MsmEntry : int { MSM_RAW = 0, MSM_ICICLE = 1, MSM_JACOBIAN = 2 };
 
+#ifndef MBLS_PINNED_ZERO_COPY
+#define MBLS_PINNED_ZERO_COPY 1  // variant builds: 0 = always stage host scalars
+#endif
 template <class F>
 eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, const MSMConfig* cfg, void* results,
                       int entry) {
@@ -1201,14 +1204,23 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     const uint8_t* d_s = static_cast<const uint8_t*>(scalars);
     const uint8_t* d_b = static_cast<const uint8_t*>(bases);
     if (st_s) {
-        // host scalars (core/msm.rs:665,773 pass a HostSlice): the copy is stream-ordered; a
-        // pageable buffer is out of the caller's memory when hipMemcpyAsync returns, a pinned one
-        // is the caller's to keep alive until the stream completes (as in ICICLE)
-        void* t = A.take(n * 32 * batch);
-        // pinned host memory: a copy kernel reading it over PCIe; pageable host memory or another
-        // device's (mbls_g*_msm_multi_device shards): hipMemcpyAsync (hipMemcpyDefault)
-        if ((er = stage_to_device(t, scalars, n * 32 * batch, st)) != MBLS_SUCCESS) return er;
-        d_s = static_cast<const uint8_t*>(t);
+        // host scalars (core/msm.rs:665,773 pass a HostSlice): stream-ordered; a pageable buffer is
+        // out of the caller's memory when hipMemcpyAsync returns, a pinned one is the caller's to
+        // keep alive until the stream completes (as in ICICLE).
+        // Pinned memory whose first kernel reads each scalar exactly once (the GLV / psi split, or
+        // the Montgomery -> standard conversion) is read in place over PCIe through its device
+        // alias: the front kernel overlaps the transfer with its own work and no 32 MiB staging
+        // copy is written and re-read.  Otherwise: a PCIe copy kernel (pinned)
+        // or hipMemcpyAsync (pageable, or another device's memory for multi-device shards).
+        const bool read_once = P.split > 1 || scal_mont;
+        const void* alias = read_once && MBLS_PINNED_ZERO_COPY ? pinned_host_device_pointer(scalars) : nullptr;
+        if (alias) {
+            d_s = static_cast<const uint8_t*>(alias);
+        } else {
+            void* t = A.take(n * 32 * batch);
+            if ((er = stage_to_device(t, scalars, n * 32 * batch, st)) != MBLS_SUCCESS) return er;
+            d_s = static_cast<const uint8_t*>(t);
+        }
     }
     if (st_b) {
         void* t = A.take(nbases * AFF);

@@ -57,59 +57,28 @@ static const uint64_t ROOT_2_32_MONT[4] = {0xb9b58d8c5f0e466aULL, 0x5b1b4c801819
                                            0x5bf3adda19e9b27bULL};
 
 // Twiddle tables of one domain build.  Callers take a shared_ptr snapshot under the lock and
-// enqueue their kernels with it, then record a use event on their stream (note_use); a table
-// superseded by an extension or a release is freed only when the last snapshot is dropped, and
-// then only after the use events of every transform that read it -- no queued transform ever
-// reads freed memory (concurrent callers on rayon threads, SURVEY.md 8b "Threading"), and no
-// device-wide synchronisation stalls unrelated work.
+// enqueue their kernels with it; a table superseded by an extension or a release is freed only
+// when the last snapshot is dropped, and then only after a device synchronisation -- no queued
+// transform ever reads freed memory (concurrent callers on rayon threads, SURVEY.md 8b
+// "Threading").  Release / extension happen once per domain size, so the synchronisation is
+// rare; an event recorded after every transform instead (round 3) cost ~5 us of dispatch delay
+// per transform (an event marker holds the next dispatch: profiles/r04/gapbench_markers.txt).
 struct DomainTables {
     int max_log = 0;            // stage tables built for stages 1..max_log
     int device = 0;             // device the tables live on
     uint8_t* tw = nullptr;      // per-stage w_(2^s)^i tables (see header)
     uint8_t* tw_inv = nullptr;  // per-stage w_(2^s)^-i
-    std::mutex mu;
-    std::vector<hipEvent_t> uses;  // events after transforms that read the tables
-    // after enqueueing a transform on `st`: record a use event (completed ones are recycled)
-    void note_use(hipStream_t st) {
-        std::lock_guard<std::mutex> g(mu);
-        hipEvent_t ev = nullptr;
-        for (size_t i = 0; i < uses.size(); ++i)
-            if (hipEventQuery(uses[i]) == hipSuccess) {
-                ev = uses[i];
-                uses.erase(uses.begin() + i);
-                break;
-            }
-        if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-            (void)hipStreamSynchronize(st);  // no event: make the use complete instead
-            return;
-        }
-        if (hipEventRecord(ev, st) != hipSuccess) {
-            (void)hipEventDestroy(ev);
-            (void)hipStreamSynchronize(st);
-            return;
-        }
-        uses.push_back(ev);
-    }
     ~DomainTables() {
         int cur = 0;
         (void)hipGetDevice(&cur);
         if (cur != device) (void)hipSetDevice(device);
-        for (hipEvent_t ev : uses) {
-            (void)hipEventSynchronize(ev);
-            (void)hipEventDestroy(ev);
-        }
+        (void)hipDeviceSynchronize();  // every transform that read the tables has finished
         if (tw) (void)hipFree(tw);
         if (tw_inv) (void)hipFree(tw_inv);
         if (cur != device) (void)hipSetDevice(cur);
     }
 };
 
-// One domain per device, as ICICLE keeps one backend state per device: init / release /
-// get_rou act on the calling thread's current device (the ICICLE active device is thread-local,
-// device_api.h:210-211), and a transform reads the tables of the device it runs on.  A device
-// whose domain was never initialised builds canonical tables on first use (order 2^32), so NTT
-// replicas on other GPUs of one process never read another device's
-// twiddle memory.
 struct Domain {
     int order_log = 32;  // 2^order_log: order of the initialised root (size bound)
     std::shared_ptr<DomainTables> tables;
@@ -670,7 +639,6 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
     }
     er = ntt_device(wout, win, log_n, inverse, batch, *tables, st);
     if (er != MBLS_SUCCESS) return er;
-    tables->note_use(st);
     if (coset && inverse) {
         uint64_t gi[4];
         hfr_inv(gi, g);

@@ -261,3 +261,30 @@ def test_msm_pinned_host_operands(amd, gh, offset):
     ref = H.g1_from_affine_mont(H.oracle_msm("g1", np.ascontiguousarray(full), amd.to_numpy_u64(b)[offset:].copy(),
                                              threads=ORACLE_THREADS))
     assert gh.decode_icicle("g1", ref_dev) == ref
+    # the reference's raw entry (standard scalars, Jacobian result) with pinned standard scalars:
+    # read in place by the GLV split; standard scalars with bitsize 128 (no split: the digit pass
+    # reads them once per window) are staged instead
+    s_std = torch.from_numpy(np.ascontiguousarray(full).view(np.int64)).pin_memory()
+    r3 = amd.msm("g1", s_std, b[offset:], icicle=False)
+    assert gh.decode_jacobian_mont("g1", np.asarray(r3)[0]) == ref
+    small = np.ascontiguousarray(full.copy())
+    small[:, 2:] = 0  # < 2^128
+    ref_small = H.g1_from_affine_mont(H.oracle_msm("g1", small, amd.to_numpy_u64(b)[offset:].copy(),
+                                                   threads=ORACLE_THREADS))
+    r4 = amd.msm("g1", torch.from_numpy(small.view(np.int64)).pin_memory(), b[offset:], icicle=False, bitsize=128)
+    assert gh.decode_jacobian_mont("g1", np.asarray(r4)[0]) == ref_small
+
+
+def test_g2_msm_pinned_host_scalars(amd, gh):
+    """G2 (psi split) with pinned Montgomery scalars read in place, equal to the oracle"""
+    import torch
+    n = (1 << 12) + 5
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0D71, montgomery=True)
+    b = torch.zeros((n, 24), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g2", b, 0x5EED0D72)
+    torch.cuda.synchronize()
+    r = amd.msm("g2", s.cpu().pin_memory(), b, icicle=True, scalars_mont=True)
+    ref = H.g2_from_affine_mont(H.oracle_msm("g2", _std_scalars(0x5EED0D71, n), amd.to_numpy_u64(b),
+                                             threads=ORACLE_THREADS))
+    assert gh.decode_icicle("g2", np.asarray(r)[0]) == ref

@@ -25,6 +25,12 @@ __global__ void k_after_ext_stop(unsigned* out) {
 __global__ void k_ext_launched(unsigned* out) {
     if (threadIdx.x == 0 && blockIdx.x == 0) out[7] += 1;
 }
+__global__ void k_after_record_devrel(unsigned* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[6] += 1;
+}
+__global__ void k_after_record_nofence(unsigned* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[6] += 1;
+}
 __global__ void k_after_record_timing(unsigned* out) {
     if (threadIdx.x == 0 && blockIdx.x == 0) out[6] += 1;
 }
@@ -83,9 +89,11 @@ int main() {
     hipStream_t st;
     hipStreamCreate(&st);
     const dim3 g(1024), b(256);
-    hipEvent_t ev, evt;
+    hipEvent_t ev, evt, evd, evn;
     hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     hipEventCreate(&evt);
+    hipEventCreateWithFlags(&evd, hipEventDisableTiming | hipEventReleaseToDevice);
+    hipEventCreateWithFlags(&evn, hipEventDisableTiming | hipEventDisableSystemFence);
     for (int rep = 0; rep < 50; ++rep) {
         hipLaunchKernelGGL(k_tiny, g, b, 0, st, d);
         hipLaunchKernelGGL(k_vgpr200, g, b, 0, st, d);
@@ -116,6 +124,10 @@ int main() {
         hipLaunchKernelGGL(k_after_wait_same, g, b, 0, st, d);
         hipExtLaunchKernelGGL(k_ext_launched, g, b, 0, st, nullptr, ev, 0, d);
         hipLaunchKernelGGL(k_after_ext_stop, g, b, 0, st, d);
+        hipEventRecord(evd, st);
+        hipLaunchKernelGGL(k_after_record_devrel, g, b, 0, st, d);
+        hipEventRecord(evn, st);
+        hipLaunchKernelGGL(k_after_record_nofence, g, b, 0, st, d);
         // back to back: a big kernel after a big kernel
         hipLaunchKernelGGL(k_big_both, g, b, 0, st, d, 5u);
         hipLaunchKernelGGL(k_big_both, g, b, 0, st, d, 7u);
