@@ -26,6 +26,14 @@ static int optimal_c(long long n) {
 
 int precompute_shift(int F) { return F > 1 ? (256 + F - 1) / F : 0; }
 
+// -DMBLS_PART_SORT=0 (variant builds) forces the tiled digits + scatter sort for every c; the
+// shipped library uses it for c > 16 only
+#ifndef MBLS_PART_SORT
+#define MBLS_PART_SORT 1
+#endif
+#ifndef SLOT0_MIN_TABLE_BYTES
+#define SLOT0_MIN_TABLE_BYTES (256ull << 20)  // the MI355X Infinity Cache (MI355X_MICROARCH.md)
+#endif
 // -DMBLS_C=<c> (tools/ variant builds) overrides the automatic window size; the caller's
 // MSMConfig.c always wins.  No run-time environment switch: a prover's environment cannot
 // select an untested schedule.
@@ -60,6 +68,17 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
         F = 1;
         if (endo == 4 && c > 16) c = 16;
     }
+    // G1 shift tables larger than the Infinity Cache (F > 2, F n 96 B > SLOT0_MIN_TABLE_BYTES): the
+    // accumulation's random point reads from the whole table cost more than the shorter tail
+    // saves (G1 2^20: factor 4 / 8 tables of 403 / 805 MB, 224 / 228 MSM/s, against 242 for the
+    // 201 MB [P, phi P] pair of the plain path, profiles/r04), so the MSM runs the plain GLV plan on
+    // slot 0 of the table (plan.bstride = F) with a compact per-call [P, phi P] table
+    p.bstride = 1;
+    if (endo == 2 && F > 2 && (size_t)n * F * 96 > SLOT0_MIN_TABLE_BYTES && MBLS_PART_SORT) {
+        p.split = 2;
+        p.bstride = F;
+        F = 1;
+    }
     // The split halves / quarters are 128 / 64-bit digit streams.  A caller's large c (picked for
     // 255-bit scalars, e.g. MIDNIGHT_MSM_WINDOW=15) can leave the top window a few bits wide: all
     // of that window's 2^21 digits (G1 2^20) then fall into a handful of buckets -- one partition
@@ -92,7 +111,7 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     p.TB = (uint32_t)Wg * p.B;
     p.chunk = CHUNK;  // msm_call replaces it with accumulate_chunk<F>(contributions)
     p.pts = (size_t)n * (p.split > 1 ? p.split : F);  // point indices (P_i, then the images)
-    p.table = p.prepared ? p.split : F;                // bases-buffer entries per point
+    p.table = p.prepared ? p.split : p.bstride > 1 ? p.bstride : F;  // bases-buffer entries per point
     p.contributions = (size_t)n * W * p.split;
     if (p.pts >= (1u << 31)) return MBLS_INVALID_ARGUMENT;
     return plan_levels(p, Wg);
@@ -724,23 +743,35 @@ __global__ __launch_bounds__(256) void k_glv_split(const uint8_t* __restrict__ s
 // -- the table no longer runs on a side stream beside the digit / sort front (its fork / join
 // event waits and its contention with k_glv_split cost more than its own time)
 template <bool MONT>
+// bstride > 1: the bases are slot 0 of a precomputed table with bstride entries per point
+// (plan.bstride, make_plan); the kernel then writes the compact [P_0..P_(n-1), phi(P_0)..] into
+// `phi` (2n rows) so the accumulation reads a 2n-point table instead of the whole precomputed one
 __global__ __launch_bounds__(256) void k_glv_prep(const uint8_t* __restrict__ scalars, uint32_t n,
                                                   uint4* __restrict__ out, ZeroList z,
-                                                  const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi) {
+                                                  const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi,
+                                                  uint32_t bstride) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     z.run(i, gridDim.x * blockDim.x);
     {  // phi rows through a 24 KB stage, written as whole lines (block_rows_out)
         __shared__ uint4 stage[256 * 6];
         const uint32_t b0 = blockIdx.x * blockDim.x;
+        const uint32_t rows = min(blockDim.x, n - b0);
+        Affine<Fq> p;
+        if (i < n) p = load_affine<Fq>(bases, (size_t)i * bstride);
+        uint8_t* phi_rows = phi;
+        if (bstride > 1) {  // the compact copy of the points first (uniform branch)
+            if (i < n) store_affine<Fq>(stage, threadIdx.x, p);
+            block_rows_out<96>(phi + (size_t)b0 * 96, stage, rows);
+            phi_rows = phi + (size_t)n * 96;
+        }
         if (i < n) {
-            Affine<Fq> p = load_affine<Fq>(bases, i);
             Fq beta;
 #pragma unroll
             for (int k = 0; k < 12; ++k) beta.v[k] = GLV_BETA_MONT[k];
             p.x = p.x * beta;
             store_affine<Fq>(stage, threadIdx.x, p);
         }
-        block_rows_out<96>(phi + (size_t)b0 * 96, stage, min(blockDim.x, n - b0));
+        block_rows_out<96>(phi_rows + (size_t)b0 * 96, stage, rows);
     }
     if (i >= n) return;
     Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
@@ -861,9 +892,11 @@ static eIcicleError digit_sources(const uint8_t* scalars, bool mont, uint32_t n,
     const SplitLayout lay = P.prepared ? SplitLayout{1u, (uint32_t)P.split} : SplitLayout{n, 1u};
     if (P.split == 2 && phi) {  // split + phi table fused (k_glv_prep)
         if (mont)
-            hipLaunchKernelGGL(k_glv_prep<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi);
+            hipLaunchKernelGGL(k_glv_prep<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi,
+                               (uint32_t)P.bstride);
         else
-            hipLaunchKernelGGL(k_glv_prep<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi);
+            hipLaunchKernelGGL(k_glv_prep<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi,
+                               (uint32_t)P.bstride);
         src = (const uint32_t*)dsrc;
         nidx = 2 * n;
     } else if (P.split == 2) {
@@ -1039,11 +1072,6 @@ static int part_fine_bits(uint32_t B) {
     return lb > 8 ? lb - 8 : 0;
 }
 
-// -DMBLS_PART_SORT=0 (variant builds) forces the tiled digits + scatter sort for every c; the
-// shipped library uses it for c > 16 only
-#ifndef MBLS_PART_SORT
-#define MBLS_PART_SORT 1
-#endif
 bool partition_sort(const MsmPlan& P) { return MBLS_PART_SORT && P.B <= DT_MAX_B; }
 
 PartSortSizes part_sort_sizes(const MsmPlan& P) {

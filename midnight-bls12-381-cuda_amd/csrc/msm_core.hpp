@@ -86,6 +86,7 @@ struct MsmPlan {
     int split;                  // endomorphism split: 1 none, 2 G1 GLV (phi), 4 G2 psi
     bool prepared;              // the bases buffer is the point-major image table (no per-call table)
     int table;                  // bases-buffer entries per point (F, or split when prepared)
+    int bstride;                // > 1: GLV plan on slot 0 of an F-entry shift table (make_plan)
     bool fq2;                   // G2 (Fq2 coordinates)
     uint32_t B, TB;
     uint32_t chunk;             // contributions per accumulation thread (accumulate_chunk)
@@ -819,7 +820,8 @@ inline uint32_t wave_min_chains(bool fq2 = false) { return fq2 ? MBLS_WAVE_MIN_G
 
 inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks) {
     MsmScratchSizes z;
-    z.phi = P.split > 1 && !P.prepared ? align_up(P.pts / P.split * (P.split - 1) * aff) : 0;
+    // the per-call image table; with bstride > 1 also the compact copy of the points (2n rows)
+    z.phi = P.split > 1 && !P.prepared ? align_up(P.pts / P.split * (P.split - 1 + (P.bstride > 1 ? 1 : 0)) * aff) : 0;
     const size_t NC = P.contributions;
     if (partition_sort(P)) {
         const PartSortSizes s = part_sort_sizes(P);
@@ -1099,8 +1101,11 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         ProfScope ps("msm.accumulate", st);
         if (img_table && !fused_table) MBLS_TRY(hipStreamWaitEvent(st, ev[1], 0));
         const uint32_t threads = (uint32_t)((NC + P.chunk - 1) / P.chunk) * LN;
+        // bstride > 1: the split kernel wrote [P; phi P] into `phi` (compact slot-0 copy)
+        const uint8_t* acc_b = P.bstride > 1 ? phi : bases;
+        const uint8_t* acc_phi = P.bstride > 1 ? phi + (size_t)n * AFF : phi;
         hipLaunchKernelGGL(accumulate_kernel<F>(), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
-                           chunk_off, first, 0u, TB, bases, phi, nsplit, P.chunk, partials);
+                           chunk_off, first, 0u, TB, acc_b, acc_phi, nsplit, P.chunk, partials);
     }
     {
         ProfScope ps("msm.bucket_sum", st);

@@ -149,3 +149,27 @@ def test_prepared_batch_per_member_tables(amd, gh):
                            threads=ORACLE_THREADS)
         assert gh.decode_icicle("g1", r[k]) == H.g1_from_affine_mont(ref), k
     del sn
+
+
+def test_large_shift_tables_take_the_slot0_glv_plan(amd, gh):
+    """G1 shift tables beyond the Infinity Cache (F n 96 B > 256 MB: factors 3, 4 and 8 at 2^20) run
+    the GLV plan on slot 0 of the table with a compact per-call [P, phi P] (make_plan bstride):
+    the benchmark inputs, Montgomery scalars, equal to the oracle"""
+    import torch
+    n = 1 << 20
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0003, montgomery=True)
+    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 0x5EED0013)
+    torch.cuda.synchronize()
+    ref = H.g1_from_affine_mont(H.oracle_msm("g1", _std_scalars(0x5EED0003, n), amd.to_numpy_u64(b),
+                                             threads=ORACLE_THREADS))
+    for F in (3, 4, 8):
+        table = torch.zeros((n * F, 12), dtype=torch.int64, device="cuda")
+        amd.precompute_bases("g1", b, F, n, out=table)
+        out = torch.zeros((1, 18), dtype=torch.int64, device="cuda")
+        amd.msm("g1", s, table, icicle=True, scalars_mont=True, points_mont=False, precompute_factor=F, out=out, n=n)
+        torch.cuda.synchronize()
+        assert gh.decode_icicle("g1", amd.to_numpy_u64(out)[0]) == ref, F
+        del table
+        torch.cuda.empty_cache()
