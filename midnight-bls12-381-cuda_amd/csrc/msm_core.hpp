@@ -351,8 +351,11 @@ MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t
 // wave's lanes run the same number of additions).  Workgroups from `light_blocks` on take the
 // heavy slices.
 template <class F>
+// 2 waves per SIMD: G1 fits anyway (181 VGPRs); G2's pair-sliced sums took 260 VGPRs + 4 AGPRs,
+// i.e. one latency-bound wave per SIMD -- capped at 256 (4 spilled) its bucket sums take 0.93
+// instead of 1.17 ms at 2^20 (A/B x2 on one box, profiles/r04/bs_minw_ab.txt)
 #ifndef MBLS_BS_MINW
-#define MBLS_BS_MINW 1
+#define MBLS_BS_MINW 2
 #endif
 __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32_t* __restrict__ chunk_off,
                                                       const uint32_t* __restrict__ perm, const uint32_t* __restrict__ binbase,
