@@ -40,14 +40,33 @@ int precompute_shift(int F) { return F > 1 ? (256 + F - 1) / F : 0; }
 #ifndef MBLS_C
 #define MBLS_C 0
 #endif
-static int auto_c(long long n) { return MBLS_C >= 2 && MBLS_C <= 20 ? MBLS_C : optimal_c(n); }
+// Split plans (round 4, tools/c_sweep.py on MI355X, profiles/r04/c_sweep.txt): the digits are
+// 128-bit (GLV) or 64-bit (psi) and the reference's classes assume 255-bit ones, so below 2^16
+// they leave the top window nearly empty (its buckets collect most digits) or too many buckets
+// for the latency-bound reduction.  Measured best windows (wall ms per call, ICICLE entry):
+//   G1 GLV: 2^8 c 8 0.71 (auto 7: 0.84); 2^13 c 10 1.07 (auto 12: 1.21); 2^14 c 11 0.97 (1.19);
+//           2^15 c 11 0.99 (13: 1.12); 2^16 c 16 1.21 (13: 1.39); >= 2^17 16
+//   G2 psi: 2^8 c 11 1.29 (7: 1.41); 2^13 c 13 1.59 (12: 2.14); 2^14 c 13 1.63 (12: 2.25);
+//           2^16 c 16 2.24 (13: 2.43); >= 2^17 16
+static int split_c(long long n, int split) {
+    if (split == 2) return n <= (1 << 11) ? 8 : n <= (1 << 13) ? 10 : n <= (1 << 15) ? 11 : 16;
+    return n <= (1 << 10) ? 11 : n <= (1 << 15) ? 13 : 16;
+}
+static int auto_c(long long n, int split) {
+    if (MBLS_C >= 2 && MBLS_C <= 20) return MBLS_C;
+    return split > 1 ? split_c(n, split) : optimal_c(n);
+}
 
 eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) {
-    int c = cfg->c > 0 ? cfg->c : auto_c(n);
-    if (c < 2 || c > 20) return MBLS_INVALID_ARGUMENT;
     int bits = cfg->bitsize > 0 ? cfg->bitsize : 255;
     if (bits > 256) return MBLS_INVALID_ARGUMENT;
     int F = cfg->precompute_factor > 0 ? cfg->precompute_factor : 1;
+    // the automatic window follows the split the plan will take (decided below with the same rules)
+    const int auto_split = (endo == 2 && (F == 2 || (F == 1 && bits > 128)))   ? 2
+                           : (endo == 4 && (F == 4 || (F == 1 && bits > 192))) ? 4
+                                                                               : 1;
+    int c = cfg->c > 0 ? cfg->c : auto_c(n, auto_split);
+    if (c < 2 || c > 20) return MBLS_INVALID_ARGUMENT;
     // Endomorphism split (no precomputed table, wide scalars):
     //   G1 GLV: two half-width digit streams, |m| < 2^127;
     //   G2 psi: four quarter-width streams, |m| < 2^63 (tiled digits only, c <= 16; worth it
