@@ -44,13 +44,15 @@ int precompute_shift(int F) { return F > 1 ? (256 + F - 1) / F : 0; }
 // 128-bit (GLV) or 64-bit (psi) and the reference's classes assume 255-bit ones, so below 2^16
 // they leave the top window nearly empty (its buckets collect most digits) or too many buckets
 // for the latency-bound reduction.  Measured best windows (wall ms per call, ICICLE entry):
-//   G1 GLV: 2^8 c 8 0.71 (auto 7: 0.84); 2^13 c 10 1.07 (auto 12: 1.21); 2^14 c 11 0.97 (1.19);
+//   G1 GLV: 2^8 c 8 0.71 (auto 7: 0.84); 2^12 c 8 0.88 (10: 0.91); 2^13 c 8 1.04 (12: 1.21);
+//           2^14 c 11 0.97 (1.19);
 //           2^15 c 11 0.99 (13: 1.12); 2^16 c 16 1.21 (13: 1.39); >= 2^17 16
-//   G2 psi: 2^8 c 11 1.29 (7: 1.41); 2^13 c 13 1.59 (12: 2.14); 2^14 c 13 1.63 (12: 2.25);
+//   G2 psi: 2^8 c 11 1.29 (7: 1.41); 2^12 c 11 1.52 (10: 1.72); 2^13 c 13 1.59 (12: 2.14);
+//           2^14 c 13 1.63 (12: 2.25);
 //           2^16 c 16 2.24 (13: 2.43); >= 2^17 16
 static int split_c(long long n, int split) {
-    if (split == 2) return n <= (1 << 11) ? 8 : n <= (1 << 13) ? 10 : n <= (1 << 15) ? 11 : 16;
-    return n <= (1 << 10) ? 11 : n <= (1 << 15) ? 13 : 16;
+    if (split == 2) return n <= (1 << 13) ? 8 : n <= (1 << 15) ? 11 : 16;
+    return n <= (1 << 12) ? 11 : n <= (1 << 15) ? 13 : 16;
 }
 static int auto_c(long long n, int split) {
     if (MBLS_C >= 2 && MBLS_C <= 20) return MBLS_C;
