@@ -11,6 +11,8 @@
 // DESIGN.md for the measured rates.
 #include <hip/hip_runtime.h>
 
+#include <optional>
+
 #include <algorithm>
 
 #include "mbls_common.hpp"
@@ -153,37 +155,43 @@ static eIcicleError run_vec_op(const mbls_fr_t* a, const mbls_fr_t* b, size_t si
     if (total == 0) return MBLS_SUCCESS;
     const size_t bytes = total * 32;
 
-    CtxLease lease(st);
-    if (!lease) return lease.error();
-    StreamCtx& ctx = *lease;
     size_t need = 0;
     if (!scalar_op && !cfg->is_a_on_device) need += align_up(bytes);
     if (!cfg->is_b_on_device) need += align_up(bytes);
     if (!cfg->is_result_on_device) need += align_up(bytes);
     if (scalar_op && !cfg->is_a_on_device) need += align_up(32 * (size_t)batch);
-    eIcicleError er = lease.reserve(need);
-    if (er != MBLS_SUCCESS) return er;
+    // device operands need no scratch: no context lease, hence no `done` event (an event marker
+    // holds the next dispatch ~5 us)
+    std::optional<CtxLease> lease;
+    Arena* arena = nullptr;
+    eIcicleError er = MBLS_SUCCESS;
+    if (need) {
+        lease.emplace(st);
+        if (!*lease) return lease->error();
+        if ((er = lease->reserve(need)) != MBLS_SUCCESS) return er;
+        arena = &(**lease).arena;
+    }
 
     const uint8_t* da = reinterpret_cast<const uint8_t*>(a);
     const uint8_t* db = reinterpret_cast<const uint8_t*>(b);
     uint8_t* dout = reinterpret_cast<uint8_t*>(output);
     if (!scalar_op && !cfg->is_a_on_device) {
-        void* t = ctx.arena.take(bytes);
+        void* t = arena->take(bytes);
         MBLS_TRY(hipMemcpyAsync(t, a, bytes, hipMemcpyHostToDevice, st));
         da = static_cast<const uint8_t*>(t);
     }
     if (!cfg->is_b_on_device) {
-        void* t = ctx.arena.take(bytes);
+        void* t = arena->take(bytes);
         MBLS_TRY(hipMemcpyAsync(t, b, bytes, hipMemcpyHostToDevice, st));
         db = static_cast<const uint8_t*>(t);
     }
-    if (!cfg->is_result_on_device) dout = static_cast<uint8_t*>(ctx.arena.take(bytes));
+    if (!cfg->is_result_on_device) dout = static_cast<uint8_t*>(arena->take(bytes));
 
     if (scalar_op) {
         // one scalar per batch entry (ICICLE v4 batched scalar ops), read on device
         const uint8_t* sv = reinterpret_cast<const uint8_t*>(a);
         if (!cfg->is_a_on_device) {
-            void* t = ctx.arena.take(32 * (size_t)batch);
+            void* t = arena->take(32 * (size_t)batch);
             MBLS_TRY(hipMemcpyAsync(t, a, 32 * (size_t)batch, hipMemcpyHostToDevice, st));
             sv = static_cast<const uint8_t*>(t);
         }
