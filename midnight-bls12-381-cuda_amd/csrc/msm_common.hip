@@ -54,9 +54,16 @@ static int split_c(long long n, int split) {
     if (split == 2) return n <= (1 << 13) ? 8 : n <= (1 << 15) ? 11 : 16;
     return n <= (1 << 12) ? 11 : n <= (1 << 15) ? 13 : 16;
 }
-static int auto_c(long long n, int split) {
+// Shift tables (precompute factor F > 1 without the split): blocks of sF = 256 / F bits.  The
+// reference's classes leave the top window of each block a few bits wide at 2^15..2^18 (c = 13 /
+// 14 against sF = 32 / 64: every block's top digits fall into a handful of buckets).  c = 16
+// divides both: G1 2^17 F = 8 1.09 ms against 3.77 with c = 14 (plain bases: 1.36), 2^18 1.54
+// against 6.69 (plain 1.74); F = 4 1.25 / 1.64 (profiles/r04/precompute_sweep.txt)
+static int auto_c(long long n, int split, int F) {
     if (MBLS_C >= 2 && MBLS_C <= 20) return MBLS_C;
-    return split > 1 ? split_c(n, split) : optimal_c(n);
+    if (split > 1) return split_c(n, split);
+    if (F > 1 && n > (1 << 12)) return 16;
+    return optimal_c(n);
 }
 
 eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) {
@@ -67,7 +74,7 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     const int auto_split = (endo == 2 && (F == 2 || (F == 1 && bits > 128)))   ? 2
                            : (endo == 4 && (F == 4 || (F == 1 && bits > 192))) ? 4
                                                                                : 1;
-    int c = cfg->c > 0 ? cfg->c : auto_c(n, auto_split);
+    int c = cfg->c > 0 ? cfg->c : auto_c(n, auto_split, F);
     if (c < 2 || c > 20) return MBLS_INVALID_ARGUMENT;
     // Endomorphism split (no precomputed table, wide scalars):
     //   G1 GLV: two half-width digit streams, |m| < 2^127;
