@@ -129,6 +129,12 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
         // may run with MIDNIGHT_MSM_WINDOW); blocks of sF bits, Wg windows each, all 256 bits
         p.sF = precompute_shift(F);
         Wg = (p.sF + c - 1) / c;
+        // automatic c: windows balanced inside the block when its top window would be nearly
+        // empty (F = 3: sF = 86, c 16 -> 15; F = 5: 52, 16 -> 13; F = 7: 37, 16 -> 13)
+        if (cfg->c <= 0 && p.sF - c * (Wg - 1) < c - 2) {
+            c = (p.sF + Wg - 1) / Wg;
+            Wg = (p.sF + c - 1) / c;
+        }
         W = F * Wg;
     }
     p.c = c;
