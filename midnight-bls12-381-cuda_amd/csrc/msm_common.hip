@@ -5,6 +5,7 @@
 // (msm_kernels.cu:69-143), histogram (:224-256), cub ExclusiveSum / SortPairs (:748-781).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <map>
 
 #include "msm_core.hpp"
@@ -54,59 +55,75 @@ static int split_c(long long n, int split) {
     if (split == 2) return n <= (1 << 13) ? 8 : n <= (1 << 15) ? 11 : 16;
     return n <= (1 << 12) ? 11 : n <= (1 << 15) ? 13 : 16;
 }
-// Shift tables (precompute factor F > 1 without the split): blocks of sF = 256 / F bits.  The
-// reference's classes leave the top window of each block a few bits wide at 2^15..2^18 (c = 13 /
-// 14 against sF = 32 / 64: every block's top digits fall into a handful of buckets).  c = 16
-// divides both: G1 2^17 F = 8 1.09 ms against 3.77 with c = 14 (plain bases: 1.36), 2^18 1.54
-// against 6.69 (plain 1.74); F = 4 1.25 / 1.64 (profiles/r04/precompute_sweep.txt)
-static int auto_c(long long n, int split, int F) {
+// Shift tables (precompute factor F > 1 run on its own blocks of sF = ceil(256 / F) bits, the
+// shift plan): a window size that leaves a block's top window a few bits wide puts that window's
+// digits into a handful of buckets (c = 14 against sF = 64: G1 2^18 F = 4 2.38 ms, c = 16 1.64),
+// and small MSMs are bound by the sort's partitions and the reduction's buckets rather than the
+// contributions.  Measured best windows (G1 / G2 wall ms per call, tools/precompute_sweep.py,
+// profiles/r04/precompute_sweep.txt):
+//   sF = 64 (F = 4):  2^8 c 8 0.58 (16: 1.52); 2^12 c 11 0.72 (16: 1.06); 2^13 c 13 0.82
+//                     (16: 1.08); 2^15 c 13 0.98 (16: 1.09); >= 2^16 16
+//   sF = 32 (F = 8):  2^10 c 11 0.53 (16: 0.86); 2^13 c 11 0.77 (16: 0.82); >= 2^14 16;
+//                     G2 2^14 c 11 1.63 (16: 1.80)
+//   sF = 16 (F = 16): 2^8 c 8 0.53 (16: 0.96); >= 2^10 16
+static int shift_c(long long n, int F, int endo) {
+    const int sF = precompute_shift(F);
+    if (sF >= 64) return n <= (1 << 8) ? 8 : n <= (1 << 12) ? 11 : n <= (1 << 15) ? 13 : 16;
+    if (sF >= 32) return n <= (endo == 4 ? (1 << 14) : (1 << 13)) ? 11 : 16;
+    if (sF >= 16) return n <= (1 << 8) ? 8 : 16;
+    return sF;
+}
+static int auto_c(long long n, int split, int F, int endo) {
     if (MBLS_C >= 2 && MBLS_C <= 20) return MBLS_C;
     if (split > 1) return split_c(n, split);
-    if (F > 1 && n > (1 << 12)) return 16;
+    if (F > 1) return shift_c(n, F, endo);
     return optimal_c(n);
+}
+
+// Which precompute factors run the shift plan.  Every contribution of a shift plan is one point
+// of one window of one block, n F ceil(sF / c) of them; the split plans take 16 n (c = 16), so
+// the shift plan gains only through its smaller bucket set (Wg windows of 2^(c-1) instead of 8),
+// and only when c divides the block: F = 4, 8, 16 (G2: 8, 16; its F = 4 is the prepared psi
+// table).  Factors 3, 5, 6, 7 lose at every size from 2^14 up (G1 2^18: 3.20 / 1.97 / 2.40 / 2.41
+// ms against 1.73 plain), G2 F = 2 and 3 too (2^14: 3.27 / 2.93 against 1.62); G1 tables past the
+// Infinity Cache (F n 96 B > SLOT0_MIN_TABLE_BYTES) lose to the GLV plan's 201 MB working set at
+// 2^20 (F = 4 / 8: 224 / 228 MSM/s against 242).  Everything else runs the group's split plan
+// on slot 0 of the table (plan.bstride = F): P_i is the table's entry i F, and the split kernel
+// writes a compact per-call [P, phi P] / [P, psi P, psi^2 P, psi^3 P].
+static bool shift_plan(long long n, int F, int endo) {
+    if (!MBLS_PART_SORT) return true;  // variant builds: no slot-0 plan without the fused front
+    if (endo == 2) return (F == 4 || F == 8 || F == 16) && (size_t)n * F * 96 <= SLOT0_MIN_TABLE_BYTES;
+    return F == 8 || F == 16;
 }
 
 eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) {
     int bits = cfg->bitsize > 0 ? cfg->bitsize : 255;
     if (bits > 256) return MBLS_INVALID_ARGUMENT;
     int F = cfg->precompute_factor > 0 ? cfg->precompute_factor : 1;
-    // the automatic window follows the split the plan will take (decided below with the same rules)
-    const int auto_split = (endo == 2 && (F == 2 || (F == 1 && bits > 128)))   ? 2
-                           : (endo == 4 && (F == 4 || (F == 1 && bits > 192))) ? 4
-                                                                               : 1;
-    int c = cfg->c > 0 ? cfg->c : auto_c(n, auto_split, F);
-    if (c < 2 || c > 20) return MBLS_INVALID_ARGUMENT;
-    // Endomorphism split (no precomputed table, wide scalars):
-    //   G1 GLV: two half-width digit streams, |m| < 2^127;
-    //   G2 psi: four quarter-width streams, |m| < 2^63 (tiled digits only, c <= 16; worth it
-    //   only for wide scalars: plain needs ceil((bits+1)/c) windows of n, psi 4 x ceil(64/c)).
-    p.split = 1;
-    p.fq2 = endo == 4;
-    p.prepared = false;
-    if (endo == 2 && F == 1 && bits > 128) p.split = 2;
-    if (endo == 4 && F == 1 && bits > 192 && c <= 16) p.split = 4;
     if (F > MAX_PRECOMPUTE) return MBLS_INVALID_ARGUMENT;
     // a precomputed table of the group's endomorphism images (precompute_factor == the split:
     // G1 2 -> [P, phi P], G2 4 -> [P, psi P, psi^2 P, psi^3 P], precompute_call) always takes the
     // split, whatever the bit size: the per-call image table is not built (DESIGN.md "prepared
-    // bases").  c only shapes the schedule: the psi digits need c <= 16.
-    if (endo > 1 && F == endo) {
-        p.split = endo;
-        p.prepared = true;
-        F = 1;
-        if (endo == 4 && c > 16) c = 16;
-    }
-    // G1 shift tables larger than the Infinity Cache (F > 2, F n 96 B > SLOT0_MIN_TABLE_BYTES): the
-    // accumulation's random point reads from the whole table cost more than the shorter tail
-    // saves (G1 2^20: factor 4 / 8 tables of 403 / 805 MB, 224 / 228 MSM/s, against 242 for the
-    // 201 MB [P, phi P] pair of the plain path, profiles/r04), so the MSM runs the plain GLV plan on
-    // slot 0 of the table (plan.bstride = F) with a compact per-call [P, phi P] table
-    p.bstride = 1;
-    if (endo == 2 && F > 2 && (size_t)n * F * 96 > SLOT0_MIN_TABLE_BYTES && MBLS_PART_SORT) {
-        p.split = 2;
-        p.bstride = F;
-        F = 1;
-    }
+    // bases").  Shift tables run the shift plan or the split plan on slot 0 (shift_plan).
+    p.prepared = endo > 1 && F == endo;
+    const bool slot0 = F > 1 && !p.prepared && !shift_plan(n, F, endo);
+    // Endomorphism split (no precomputed table, wide scalars):
+    //   G1 GLV: two half-width digit streams, |m| < 2^127;
+    //   G2 psi: four quarter-width streams, |m| < 2^63 (tiled digits only, c <= 16; worth it
+    //   only for wide scalars: plain needs ceil((bits+1)/c) windows of n, psi 4 x ceil(64/c)).
+    const bool wide = endo == 2 ? bits > 128 : bits > 192;
+    const int split = endo > 1 && (p.prepared || slot0 || (F == 1 && wide)) ? endo : 1;
+    int c = cfg->c > 0 ? cfg->c : auto_c(n, split, split > 1 ? 1 : F, endo);
+    if (c < 2 || c > 20) return MBLS_INVALID_ARGUMENT;
+    p.split = 1;
+    p.fq2 = endo == 4;
+    if (split == 2) p.split = 2;
+    // the psi digits need c <= 16: a plain-bases MSM with a larger c stays unsplit, a table's
+    // schedule (c only shapes it) runs with 16
+    if (split == 4 && (c <= 16 || F > 1)) p.split = 4;
+    if (p.split == 4 && c > 16) c = 16;
+    p.bstride = slot0 ? F : 1;
+    if (p.split > 1 && F > 1) F = 1;
     // The split halves / quarters are 128 / 64-bit digit streams.  A caller's large c (picked for
     // 255-bit scalars, e.g. MIDNIGHT_MSM_WINDOW=15) can leave the top window a few bits wide: all
     // of that window's 2^21 digits (G1 2^20) then fall into a handful of buckets -- one partition
@@ -130,7 +147,8 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
         p.sF = precompute_shift(F);
         Wg = (p.sF + c - 1) / c;
         // automatic c: windows balanced inside the block when its top window would be nearly
-        // empty (F = 3: sF = 86, c 16 -> 15; F = 5: 52, 16 -> 13; F = 7: 37, 16 -> 13)
+        // empty (-DMBLS_PART_SORT=0 variant builds, where every factor runs the shift plan:
+        // F = 3: sF = 86, c 16 -> 15; F = 5: 52, 16 -> 13; F = 7: 37, 16 -> 13)
         if (cfg->c <= 0 && p.sF - c * (Wg - 1) < c - 2) {
             c = (p.sF + Wg - 1) / Wg;
             Wg = (p.sF + c - 1) / c;
@@ -653,13 +671,27 @@ MBLS_DEV void psi_images(const Affine<Fq2>& p, Affine<Fq2>& q1, Affine<Fq2>& q2,
     q3 = Affine<Fq2>{Fq2{q1.x.c0 * c2, q1.x.c1 * c2}, neg(q1.y)};
 }
 
-// the block's rows of the three psi tables (table j at (j - 1) n), through one 48 KB stage
-MBLS_DEV void psi_block(const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi, uint32_t n) {
+// the block's rows of the three psi tables (table j at (j - 1) n), through one 48 KB stage.
+// bstride > 1: the bases are slot 0 of a precomputed table with bstride entries per point
+// (plan.bstride); the compact copy of the points goes first, [P, psi P, psi^2 P, psi^3 P] (4n rows)
+MBLS_DEV void psi_block(const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi, uint32_t n,
+                        uint32_t bstride = 1) {
     __shared__ uint4 stage[256 * 12];
     const uint32_t b0 = blockIdx.x * blockDim.x, i = b0 + threadIdx.x;
     const uint32_t rows = min(blockDim.x, n - b0);
     Affine<Fq2> q[3];
-    if (i < n) psi_images(load_affine<Fq2>(bases, i), q[0], q[1], q[2]);
+    if (bstride > 1) {  // uniform branch
+        Affine<Fq2> p;
+        if (i < n) {
+            p = load_affine<Fq2>(bases, (size_t)i * bstride);
+            store_affine<Fq2>(stage, threadIdx.x, p);
+            psi_images(p, q[0], q[1], q[2]);
+        }
+        block_rows_out<192>(phi + (size_t)b0 * 192, stage, rows);
+        phi += (size_t)n * 192;
+    } else if (i < n) {
+        psi_images(load_affine<Fq2>(bases, i), q[0], q[1], q[2]);
+    }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         if (i < n) store_affine<Fq2>(stage, threadIdx.x, q[j]);
@@ -677,10 +709,11 @@ __global__ __launch_bounds__(256) void k_psi_table(const uint8_t* __restrict__ b
 template <bool MONT>
 __global__ __launch_bounds__(256) void k_psi_prep(const uint8_t* __restrict__ scalars, uint32_t n,
                                                   uint4* __restrict__ out, ZeroList z,
-                                                  const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi) {
+                                                  const uint8_t* __restrict__ bases, uint8_t* __restrict__ phi,
+                                                  uint32_t bstride) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     z.run(i, gridDim.x * blockDim.x);
-    psi_block(bases, phi, n);  // every thread (block barriers)
+    psi_block(bases, phi, n, bstride);  // every thread (block barriers)
     if (i >= n) return;
     psi_split_one<MONT>(scalars, n, out, i, SplitLayout{n, 1});
 }
@@ -942,9 +975,11 @@ static eIcicleError digit_sources(const uint8_t* scalars, bool mont, uint32_t n,
         nidx = 2 * n;
     } else if (P.split == 4 && phi) {  // split + psi table fused (k_psi_prep)
         if (mont)
-            hipLaunchKernelGGL(k_psi_prep<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi);
+            hipLaunchKernelGGL(k_psi_prep<true>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi,
+                               (uint32_t)P.bstride);
         else
-            hipLaunchKernelGGL(k_psi_prep<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi);
+            hipLaunchKernelGGL(k_psi_prep<false>, g, dim3(256), 0, st, scalars, n, (uint4*)dsrc, z, bases, phi,
+                               (uint32_t)P.bstride);
         src = (const uint32_t*)dsrc;
         nidx = 4 * n;
     } else if (P.split == 4) {
@@ -1122,18 +1157,29 @@ PartSortSizes part_sort_sizes(const MsmPlan& P) {
     return s;
 }
 
-// Signed digits of uniform windows (sF == 0) in closed form: with C = sum_w (B - 1) 2^(c w), the
-// base-2^c digits e_w of s + C give d_w = e_w - (B - 1) in [1 - B, B] -- the unique signed
-// representation with that digit range, so exactly digit_at's carry-chain digits, without its
-// loop over the lower windows (O(w) per digit).  s + C < 2^(c W) for the window counts
-// make_plan picks (no final carry); NW + 1 words hold it.
+// Signed digits in closed form: with C = sum (B - 1) 2^pos_w over the full-width windows w, the
+// bits e_w of s + C at window w's span (window_span) give d_w = e_w - (B - 1) in [1 - B, B] for a
+// full window -- the unique signed representation with that digit range, so exactly digit_at's
+// carry-chain digits, without its loop over the lower windows (O(w) per digit) -- and d_w = e_w
+// for the narrower top window of a shift-table block (sF not a multiple of c), which never
+// carries in the chain.  The two representations differ only where a narrow window's digits and
+// carry add up to 2^wid (the chain's digit 2^wid, here 0 and one more in the next block); both
+// sum to s, and the result is the same point.  s + C < 2^(c W) (uniform windows) or 2^256 (shift
+// tables: s < 2^255 and C's top term is below 2^255) for the plans make_plan picks; NW + 1 words
+// hold it.
 struct DigitOffset {
     uint32_t w[9];
 };
-static DigitOffset digit_offset(int c, int W, uint32_t B) {
+static DigitOffset digit_offset(int c, int W, uint32_t B, int Wg, int sF) {
     DigitOffset o{};
     for (int j = 0; j < W; ++j) {
-        const int pos = c * j;
+        int pos = c * j, wid = c;
+        if (sF) {
+            const int f = j / Wg, l = j - f * Wg;
+            pos = sF * f + c * l;
+            wid = std::min(c, sF - c * l);
+        }
+        if (wid != c) continue;
         const uint64_t v = (uint64_t)(B - 1) << (pos & 31);
         const int k = pos >> 5;
         if (k < 9) o.w[k] += (uint32_t)v;  // windows do not overlap: no carries between terms
@@ -1142,20 +1188,24 @@ static DigitOffset digit_offset(int c, int W, uint32_t B) {
     return o;
 }
 template <int NW>
-MBLS_DEV uint32_t digit_closed(const uint32_t (&x)[NW], const DigitOffset& C, int w, int c, uint32_t B) {
+MBLS_DEV uint32_t digit_closed(const uint32_t (&x)[NW], const DigitOffset& C, int w, int c, uint32_t B, int Wg,
+                               int sF) {
     uint32_t y[NW + 1];
     unsigned carry = 0;
 #pragma unroll
     for (int k = 0; k < NW; ++k) y[k] = __builtin_addc(x[k], C.w[k], carry, &carry);
     y[NW] = C.w[NW] + carry;
-    const int bit = c * w, word = bit >> 5, sh = bit & 31;
+    int bit, wid;
+    window_span(w, c, Wg, sF, bit, wid);
+    const int word = bit >> 5, sh = bit & 31;
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int k = 0; k <= NW; ++k) {
         lo = (k == word) ? y[k] : lo;
         hi = (k == word + 1) ? y[k] : hi;
     }
-    const uint32_t e = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & ((1u << c) - 1);
+    const uint32_t e = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & ((1u << wid) - 1);
+    if (wid != c) return e;  // a block's narrow top window
     // d = e - (B - 1): positive (e >= B - 1) or -(B - 1 - e), as magnitude | sign bit
     return e >= B - 1 ? e - (B - 1) : ((B - 1 - e) | 0x80000000u);
 }
@@ -1200,7 +1250,7 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __re
                 negh = x[3] >> 31;
                 x[3] &= 0x7fffffffu;
             }
-            const uint32_t d = (sF == 0 ? digit_closed<NW>(x, C, w, c, B) : digit_at<NW>(x, w, c, B, Wg, sF)) ^ (negh << 31);
+            const uint32_t d = digit_closed<NW>(x, C, w, c, B, Wg, sF) ^ (negh << 31);
             dig[k] = d;
             if (d & 0x7fffffffu) lr[k] = atomicAdd(&hist[((d & 0x7fffffffu) - 1) >> FB], 1u);
         }
@@ -1485,7 +1535,7 @@ eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, c
     if (er != MBLS_SUCCESS) return er;
     dim3 g(z.segments), b(DT_THREADS);
     const uint32_t F = (uint32_t)P.F;
-    const DigitOffset C = digit_offset(P.c, P.W, P.B);
+    const DigitOffset C = digit_offset(P.c, P.W, P.B, P.Wg, P.sF);
 #define MBLS_DP(S_, P_)                                                                                           \
     hipLaunchKernelGGL((k_digits_part<S_, P_>), g, b, 0, st, src, nidx, P.c, P.Wg, P.sF, F, P.B, z.FB, z.NP, ent, seg_off, \
                        seg_cnt, part_tot, C)

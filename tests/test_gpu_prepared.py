@@ -173,3 +173,35 @@ def test_large_shift_tables_take_the_slot0_glv_plan(amd, gh):
         assert gh.decode_icicle("g1", amd.to_numpy_u64(out)[0]) == ref, F
         del table
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("group,n,factors", [
+    ("g1", 200, (3, 4, 8, 16, 32)),
+    ("g1", 5000, (3, 4, 5, 6, 7, 8, 16)),
+    ("g1", (1 << 13) + 3, (4, 8, 16)),
+    ("g2", 200, (2, 3, 8, 16)),
+    ("g2", 3000, (2, 3, 5, 8, 16)),
+])
+def test_shift_and_slot0_plans(amd, gh, group, n, factors):
+    """every precompute factor, whichever plan make_plan picks for it (shift plan with the
+    measured windows for F = 4 / 8 / 16, the split plan on slot 0 of the table for the others),
+    full-width and 64-bit scalars and a caller's c, equal to the oracle"""
+    import torch
+    w = 12 if group == "g1" else 24
+    g = pr.rng(40 + n)
+    sc = [g.randrange(pr.R) for _ in range(n)]
+    b = torch.zeros((n, w), dtype=torch.int64, device="cuda")
+    amd.gen_bases(group, b, 0x5EED0F10 + n)
+    bn = amd.to_numpy_u64(b)
+    dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
+    cases = []
+    for bits in (0, 64):
+        vals = sc if bits == 0 else [x % (1 << 64) for x in sc]
+        s = H.ints_to_limbs(vals, 4)
+        cases.append((bits, s, dec(H.oracle_msm(group, s, bn, threads=ORACLE_THREADS))))
+    for F in factors:
+        table = amd.precompute_bases(group, b, F, n)
+        for bits, s, ref in cases:
+            for c in ((0, 13) if bits == 0 else (0,)):
+                r = amd.msm(group, s, table, c=c, bitsize=bits, precompute_factor=F, n=n)
+                assert gh.decode_icicle(group, r[0]) == ref, (F, bits, c)
