@@ -302,6 +302,14 @@ eIcicleError mbls_g2_msm_multi_device(const mbls_fr_t* scalars, const mbls_g2_af
  * batch_size sums of `size` elements, row-major batches; result host or device). */
 eIcicleError bls12_381_vector_sum(const mbls_fr_t* a, size_t size, const VecOpsConfig* config, mbls_fr_t* output);
 
+/* The MSM schedule the library picks for msm_size points under `config` (make_plan; host
+ * only, no device work): out[0..9] = window bits c, windows W, windows per table block Wg, the
+ * plan's precompute factor F (1 once a split plan takes the table), block shift sF (0: none),
+ * split (1 none, 2 G1 GLV, 4 G2 psi), prepared endomorphism table (0 / 1), slot-0 stride (1:
+ * none; F: the split plan on entry i F of a shift table), buckets, reduction levels.
+ * group: 1 = G1, 2 = G2.  Diagnostics (tests/test_plan.py, tools/). */
+eIcicleError mbls_msm_plan(int group, int msm_size, const MSMConfig* config, int32_t* out);
+
 /* Stage profiler (tracing): hipEvent pairs recorded on the caller's
  * stream around each pipeline stage ("msm.accumulate", "ntt.pass", ...) when enabled
  * (or MBLS_PROFILE=1).  read() synchronises the recorded events and returns, per stage,

@@ -77,6 +77,7 @@ EXPORTED = [
     "mbls_release_stream", "mbls_release_scratch", "mbls_scratch_stats",
     "mbls_g1_msm_multi_device", "mbls_g2_msm_multi_device", "bls12_381_vector_sum",
     "bls12_381_g1_affine_to_projective", "bls12_381_g1_projective_to_affine", "bls12_381_g2_projective_to_affine",
+    "mbls_msm_plan",
 ]
 
 _LIB = None
@@ -119,6 +120,7 @@ def lib():
         "bls12_381_vector_sum": [P, sz, P, P],
         "bls12_381_g1_affine_to_projective": [P, i32, P, P], "bls12_381_g1_projective_to_affine": [P, i32, P, P],
         "bls12_381_g2_projective_to_affine": [P, i32, P, P],
+        "mbls_msm_plan": [i32, i32, P, P],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -196,6 +198,17 @@ def msm_config(**kw):
         else:
             setattr(c, k, v)
     return c
+
+
+PLAN_FIELDS = ("c", "W", "Wg", "F", "sF", "split", "prepared", "bstride", "buckets", "levels")
+
+
+def msm_plan(group, n, **cfg):
+    """the MSM schedule the library picks (mbls_msm_plan; host only): dict of PLAN_FIELDS"""
+    out = (ctypes.c_int32 * len(PLAN_FIELDS))()
+    c = msm_config(**cfg)
+    check(lib().mbls_msm_plan(1 if group == "g1" else 2, n, ctypes.byref(c), out), "msm_plan")
+    return dict(zip(PLAN_FIELDS, list(out)))
 
 
 def ntt_config(**kw):

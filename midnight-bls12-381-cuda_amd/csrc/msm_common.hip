@@ -169,6 +169,21 @@ eIcicleError make_plan(long long n, const MSMConfig* cfg, MsmPlan& p, int endo) 
     return plan_levels(p, Wg);
 }
 
+}  // namespace mbls
+
+extern "C" eIcicleError mbls_msm_plan(int group, int msm_size, const MSMConfig* config, int32_t* out) {
+    if (!config || !out) return MBLS_INVALID_POINTER;
+    if ((group != 1 && group != 2) || msm_size < 0) return MBLS_INVALID_ARGUMENT;
+    mbls::MsmPlan p;
+    const eIcicleError er = mbls::make_plan(msm_size > 0 ? msm_size : 1, config, p, group == 1 ? 2 : 4);
+    if (er != MBLS_SUCCESS) return er;
+    const int32_t v[10] = {p.c, p.W, p.Wg, p.F, p.sF, p.split, p.prepared ? 1 : 0, p.bstride, (int32_t)p.TB, p.levels};
+    for (int k = 0; k < 10; ++k) out[k] = v[k];
+    return MBLS_SUCCESS;
+}
+
+namespace mbls {
+
 // Reduction levels for launches over Wl windows: level 0 has B inputs, level l divides by
 // 2^seg_log[l], the last has one output.  A level with many segments runs one per LANE, fewer
 // one per 16-lane ROW, few one per WAVE with shorter segments.  The -DMBLS_ROW_SEG_LOG /
