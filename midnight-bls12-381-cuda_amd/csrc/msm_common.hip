@@ -33,7 +33,7 @@ int precompute_shift(int F) { return F > 1 ? (256 + F - 1) / F : 0; }
 #define MBLS_PART_SORT 1
 #endif
 #ifndef SLOT0_MIN_TABLE_BYTES
-#define SLOT0_MIN_TABLE_BYTES (256ull << 20)  // the MI355X Infinity Cache (MI355X_MICROARCH.md)
+#define SLOT0_MIN_TABLE_BYTES (1ull << 30)  // G1 shift tables above run the GLV plan on slot 0 (shift_plan)
 #endif
 // -DMBLS_C=<c> (tools/ variant builds) overrides the automatic window size; the caller's
 // MSMConfig.c always wins.  No run-time environment switch: a prover's environment cannot
@@ -85,9 +85,10 @@ static int auto_c(long long n, int split, int F, int endo) {
 // the shift plan gains only through its smaller bucket set (Wg windows of 2^(c-1) instead of 8),
 // and only when c divides the block: F = 4, 8, 16 (G2: 8, 16; its F = 4 is the prepared psi
 // table).  Factors 3, 5, 6, 7 lose at every size from 2^14 up (G1 2^18: 3.20 / 1.97 / 2.40 / 2.41
-// ms against 1.73 plain), G2 F = 2 and 3 too (2^14: 3.27 / 2.93 against 1.62); G1 tables past the
-// Infinity Cache (F n 96 B > SLOT0_MIN_TABLE_BYTES) lose to the GLV plan's 201 MB working set at
-// 2^20 (F = 4 / 8: 224 / 228 MSM/s against 242).  Everything else runs the group's split plan
+// ms against 1.73 plain), G2 F = 2 and 3 too (2^14: 3.27 / 2.93 against 1.62).  G1 tables above
+// 1 GiB (F n 96 B > SLOT0_MIN_TABLE_BYTES) lose to the GLV plan's 201 MB working set: 2^20 F = 16
+// (1.6 GB) 4.17 ms against 4.13, while the 805 MB F = 8 table still wins (3.92; 2^19 F = 16 2.37
+// against 2.56).  Everything else runs the group's split plan
 // on slot 0 of the table (plan.bstride = F): P_i is the table's entry i F, and the split kernel
 // writes a compact per-call [P, phi P] / [P, psi P, psi^2 P, psi^3 P].
 static bool shift_plan(long long n, int F, int endo) {

@@ -151,10 +151,11 @@ def test_prepared_batch_per_member_tables(amd, gh):
     del sn
 
 
-def test_large_shift_tables_take_the_slot0_glv_plan(amd, gh):
-    """G1 shift tables beyond the Infinity Cache (F n 96 B > 256 MB: factors 3, 4 and 8 at 2^20) run
-    the GLV plan on slot 0 of the table with a compact per-call [P, phi P] (make_plan bstride):
-    the benchmark inputs, Montgomery scalars, equal to the oracle"""
+def test_large_shift_tables_at_2e20(amd, gh):
+    """G1 tables at 2^20 through every plan make_plan has for them: F = 3 and 16 (1.6 GB, above
+    1 GiB) run the GLV plan on slot 0 of the table with a compact per-call [P, phi P] (make_plan
+    bstride), F = 4 and 8 (403 / 805 MB) the shift plan; the benchmark inputs, Montgomery
+    scalars, equal to the oracle"""
     import torch
     n = 1 << 20
     s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
@@ -164,7 +165,7 @@ def test_large_shift_tables_take_the_slot0_glv_plan(amd, gh):
     torch.cuda.synchronize()
     ref = H.g1_from_affine_mont(H.oracle_msm("g1", _std_scalars(0x5EED0003, n), amd.to_numpy_u64(b),
                                              threads=ORACLE_THREADS))
-    for F in (3, 4, 8):
+    for F in (3, 4, 8, 16):
         table = torch.zeros((n * F, 12), dtype=torch.int64, device="cuda")
         amd.precompute_bases("g1", b, F, n, out=table)
         out = torch.zeros((1, 18), dtype=torch.int64, device="cuda")

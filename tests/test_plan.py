@@ -56,9 +56,9 @@ def test_prepared_tables_take_the_split(amd, group, F):
     assert amd.msm_plan("g2", 1 << 16, precompute_factor=4, c=18)["c"] == 16
 
 
-@pytest.mark.parametrize("F,log_n,c", [(4, 8, 8), (4, 12, 11), (4, 14, 13), (4, 16, 16), (4, 19, 16),
-                                       (8, 10, 11), (8, 13, 11), (8, 14, 16), (8, 18, 16),
-                                       (16, 8, 8), (16, 10, 16), (16, 17, 16)])
+@pytest.mark.parametrize("F,log_n,c", [(4, 8, 8), (4, 12, 11), (4, 14, 13), (4, 16, 16), (4, 20, 16), (4, 21, 16),
+                                       (8, 10, 11), (8, 13, 11), (8, 14, 16), (8, 20, 16),
+                                       (16, 8, 8), (16, 10, 16), (16, 19, 16)])
 def test_g1_shift_plans_and_windows(amd, F, log_n, c):
     p = amd.msm_plan("g1", 1 << log_n, precompute_factor=F)
     sF = (256 + F - 1) // F
@@ -66,9 +66,9 @@ def test_g1_shift_plans_and_windows(amd, F, log_n, c):
     assert p["Wg"] == (sF + c - 1) // c and p["W"] == F * p["Wg"]
 
 
-@pytest.mark.parametrize("F,log_n", [(4, 20), (8, 19), (8, 20), (16, 18), (16, 24)])
-def test_g1_shift_tables_past_the_infinity_cache_run_slot0(amd, F, log_n):
-    assert (1 << log_n) * F * 96 > 256 << 20
+@pytest.mark.parametrize("F,log_n", [(4, 22), (8, 21), (16, 20), (16, 24)])
+def test_g1_shift_tables_above_1gib_run_slot0(amd, F, log_n):
+    assert (1 << log_n) * F * 96 > 1 << 30
     p = amd.msm_plan("g1", 1 << log_n, precompute_factor=F)
     assert (p["split"], p["bstride"], p["F"], p["c"]) == (2, F, 1, 16)
 
