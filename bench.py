@@ -48,7 +48,7 @@ PROFILES = os.path.join(ROOT, "profiles")
 
 
 def pmc_summary():
-    for rnd in ("r03", "r02", "r01"):
+    for rnd in ("r04/closing", "r03", "r02", "r01"):
         path = os.path.join(PROFILES, rnd, "pmc_summary.json")
         try:
             with open(path) as f:
