@@ -186,13 +186,21 @@ def test_large_shift_tables_at_2e20(amd, gh):
 def test_shift_and_slot0_plans(amd, gh, group, n, factors):
     """every precompute factor, whichever plan make_plan picks for it (shift plan with the
     measured windows for F = 4 / 8 / 16, the split plan on slot 0 of the table for the others),
-    full-width and 64-bit scalars and a caller's c, equal to the oracle"""
+    full-width and 64-bit scalars and a caller's c, edge scalars and equal points, equal to the
+    oracle"""
     import torch
     w = 12 if group == "g1" else 24
     g = pr.rng(40 + n)
-    sc = [g.randrange(pr.R) for _ in range(n)]
+    # block and window boundaries of every table shape (2^16 k - 1, 2^(sF f)), the split
+    # boundaries, and one scalar repeated 40 times (a heavy bucket in every window)
+    edge = (H.glv_edge_scalars() if group == "g1" else H.psi_edge_scalars()) + \
+        [(1 << k) - 1 for k in (8, 11, 13, 16, 32, 37, 43, 52, 64, 86, 128, 172, 192, 240)] + \
+        [1 << k for k in (16, 32, 64, 128, 192, 240)] + [0x5EED << 100] * 40
+    sc = [x % pr.R for x in edge][:n] + [g.randrange(pr.R) for _ in range(max(0, n - len(edge)))]
     b = torch.zeros((n, w), dtype=torch.int64, device="cuda")
     amd.gen_bases(group, b, 0x5EED0F10 + n)
+    b[1] = b[0]  # equal points: a doubling inside a bucket chain
+    b[3] = b[2]
     bn = amd.to_numpy_u64(b)
     dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
     cases = []
