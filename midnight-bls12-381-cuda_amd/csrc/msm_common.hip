@@ -1358,8 +1358,56 @@ static constexpr uint32_t PS_RS = 8, PS_RK = 6;
 #endif
 static constexpr bool PS_KEEP = MBLS_PS_KEEP != 0;
 
+// rank of this lane's entry in LDS counter cnt[key]: one atomic per wave when its active lanes
+// share the key (skewed scalars: a heavy part's entries all in one fine bucket, whose per-lane
+// atomics serialised -- G1 2^20 with every scalar 1: k_part_sort 2.1 ms), else one per lane.
+// Ranks inside a bucket follow lane order, which only permutes the bucket's summands.
+MBLS_DEV uint32_t lds_rank(uint32_t* cnt, uint32_t key) {
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+    const uint64_t act = __ballot(1);
+    if (__ballot(key == k0) == act) {
+        const uint32_t leader = (uint32_t)__builtin_ctzll(act);
+        uint32_t base = 0;
+        if (__lane_id() == leader) base = atomicAdd(&cnt[k0], (uint32_t)__popcll(act));
+        base = __shfl(base, leader, 64);
+        return base + (uint32_t)__popcll(act & ((1ull << __lane_id()) - 1));
+    }
+    return atomicAdd(&cnt[key], 1u);
+}
+
+// the entries of one segment's part (k of them from ent[o]), PS_U loads in flight per lane (a
+// heavy part's workgroup walks up to 2^20 entries: one load latency per entry was its bound)
+#ifndef MBLS_PS_U
+#define MBLS_PS_U 4
+#endif
+static constexpr uint32_t PS_U = MBLS_PS_U;
+template <bool PACK, class Fn>
+MBLS_DEV void part_walk(const uint32_t* __restrict__ ent, size_t o, uint32_t k, uint32_t tl, int FB, Fn&& fn) {
+    for (uint32_t i = tl; i < k; i += PS_U * PS_TEAM) {
+        uint32_t fine[PS_U], val[PS_U];
+#pragma unroll
+        for (uint32_t u = 0; u < PS_U; ++u) {
+            fine[u] = val[u] = 0;
+            if (i + u * PS_TEAM < k) part_entry<PACK>(ent, o + i + u * PS_TEAM, FB, fine[u], val[u]);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PS_U; ++u)
+            if (i + u * PS_TEAM < k) fn(fine[u], val[u]);
+    }
+}
+
+// workgroup size of k_part_sort: a heavy part (skewed scalars) is walked by one workgroup, whose
+// dependent LDS ranks are latency-bound at four waves.  1024 threads (G1 2^20, tools/skew_probe.py):
+// every scalar 1 3.57 -> 1.78 ms, 8-bit scalars 2.38 -> 1.71, half ones 4.36 -> 3.55; random
+// scalars unchanged (4.26-4.37 / 4.28-4.30)
+#ifndef MBLS_PS_THREADS
+#define MBLS_PS_THREADS 1024
+#endif
+static constexpr uint32_t PS_THREADS = MBLS_PS_THREADS;
+static_assert(PS_THREADS % 64 == 0 && PS_THREADS <= 1024 && PS_THREADS >= 256, "MBLS_PS_THREADS");
+
 template <bool PACK>
-__global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ ent, const uint32_t* __restrict__ seg_off,
+__global__ __launch_bounds__(PS_THREADS) void k_part_sort(const uint32_t* __restrict__ ent, const uint32_t* __restrict__ seg_off,
                                                    const uint32_t* __restrict__ seg_cnt,
                                                    const uint32_t* __restrict__ part_tot, uint32_t tiles, int W,
                                                    int Wg, uint32_t B, int FB, uint32_t NP,
@@ -1371,7 +1419,7 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
     const uint32_t wl = blockIdx.x / NP, part = blockIdx.x % NP;
     // windows of group wl: wl, wl + Wg, ... < W (precompute factor F > 1), `tiles` segments each
     const uint32_t S = ((uint32_t)(W - 1 - (int)wl) / (uint32_t)Wg + 1) * tiles;
-    const uint32_t team = threadIdx.x / PS_TEAM, tl = threadIdx.x % PS_TEAM, nteams = 256 / PS_TEAM;
+    const uint32_t team = threadIdx.x / PS_TEAM, tl = threadIdx.x % PS_TEAM, nteams = PS_THREADS / PS_TEAM;
     if (threadIdx.x < FBN) cnt[threadIdx.x] = 0;
     if (threadIdx.x < ORDER_BINS) chist[threadIdx.x] = 0;
     __syncthreads();
@@ -1413,24 +1461,21 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
             const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
             const uint32_t k = seg_cnt[seg * NP + part];
             const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
-            for (uint32_t i = tl; i < k; i += PS_TEAM) {
-                uint32_t fine, val;
-                part_entry<PACK>(ent, o + i, FB, fine, val);
-                atomicAdd(&cnt[fine], 1u);
-            }
+            part_walk<PACK>(ent, o, k, tl, FB, [&](uint32_t fine, uint32_t) { lds_rank(cnt, fine); });
         }
     }
     // this part's base: the sum of the part totals before it (blockIdx = wl * NP + part, the
     // scan order); block 0 sums them all for offsets[Wg B].  <= Wg * NP = 2048 words: cheaper
     // than the three launches of a separate scan
-    __shared__ uint32_t wsum[4];
+    constexpr uint32_t NWV = PS_THREADS / 64, PJ = 2048 / PS_THREADS;
+    __shared__ uint32_t wsum[NWV];
     {
         const uint32_t lim = blockIdx.x == 0 ? (uint32_t)Wg * NP : blockIdx.x;
         uint32_t a = 0;
-        if (lim <= 8 * 256) {  // independent loads (the strided loop waited one latency per step)
+        if (lim <= PJ * PS_THREADS) {  // independent loads (the strided loop waited one latency per step)
 #pragma unroll
-            for (uint32_t j = 0; j < 8; ++j) {
-                const uint32_t k = threadIdx.x + 256 * j;
+            for (uint32_t j = 0; j < PJ; ++j) {
+                const uint32_t k = threadIdx.x + PS_THREADS * j;
                 a += k < lim ? part_tot[k] : 0u;
             }
         } else {
@@ -1440,7 +1485,9 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
         if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = a;
     }
     __syncthreads();
-    const uint32_t psum = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    uint32_t psum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NWV; ++k) psum += wsum[k];
     const uint32_t base = blockIdx.x == 0 ? 0u : psum;
     if (threadIdx.x < 64) {  // wave 0: exclusive scan of the FBN <= 128 fine counts, 2 per lane
         const uint32_t l = threadIdx.x;
@@ -1498,7 +1545,7 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
     const uint32_t span = span_sh;
     const bool staged = span <= PS_STAGE;
     auto place = [&](uint32_t fine, uint32_t val) {
-        const uint32_t pos = pre[fine] + atomicAdd(&cnt[fine], 1u);
+        const uint32_t pos = pre[fine] + lds_rank(cnt, fine);
         if (staged)
             ps_stage[pos] = val;
         else
@@ -1519,11 +1566,7 @@ __global__ __launch_bounds__(256) void k_part_sort(const uint32_t* __restrict__ 
             const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
             const uint32_t k = seg_cnt[seg * NP + part];
             const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
-            for (uint32_t i = tl; i < k; i += PS_TEAM) {
-                uint32_t fine, val;
-                part_entry<PACK>(ent, o + i, FB, fine, val);
-                place(fine, val);
-            }
+            part_walk<PACK>(ent, o, k, tl, FB, place);
         }
     }
     if (staged) {  // workgroup-uniform
@@ -1576,7 +1619,7 @@ eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint3
                               const ChunkCountOut& cc, hipStream_t st) {
     const PartSortSizes z = part_sort_sizes(P);
     if (cc.nchunks && z.FB != CHUNK_FUSED_SHIFT) return MBLS_INVALID_ARGUMENT;
-    dim3 g((uint32_t)P.Wg * z.NP), b(256);
+    dim3 g((uint32_t)P.Wg * z.NP), b(PS_THREADS);
     if (z.pack)
         hipLaunchKernelGGL(k_part_sort<true>, g, b, 0, st, ent, seg_off, seg_cnt, part_tot, z.tiles, P.W, P.Wg, P.B,
                            z.FB, z.NP, counts, offsets, sorted, cc);
@@ -1753,17 +1796,36 @@ __global__ __launch_bounds__(256) void k_chunk_owner(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ binbase, uint32_t* __restrict__ perm,
                                                      HeavyTab H) {
     __shared__ uint32_t cur[ORDER_BINS];
+    // long owner / first ranges (heavy buckets: skewed scalars put up to 2^16 chunks in one
+    // bucket, whose lone thread took 2.75 ms to write them at G1 2^20) are queued and written by
+    // the whole workgroup
+    __shared__ uint32_t qn, qk0[256], qk1[256], qt0[256], qt1[256], qb[256];
     if (threadIdx.x < ORDER_BINS) cur[threadIdx.x] = binbase[order_index(blockIdx.x, threadIdx.x, gridDim.x)];
+    if (threadIdx.x == 0) qn = 0;
     __syncthreads();
-    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < m) {
+        const uint32_t k0 = cloc[b] + blk_pre[b >> cs];
+        const uint32_t k1 = b + 1 < m ? cloc[b + 1] + blk_pre[(b + 1) >> cs] : blk_pre[(m + (1u << cs) - 1) >> cs];
+        chunk_off[b] = k0;
+        if (b + 1 == m) chunk_off[m] = k1;
+        const uint32_t o = offsets[b], e = offsets[b + 1];
+        const uint32_t t0 = (o + L - 1) / L, t1 = (e + L - 1) / L;
+        if (k1 - k0 > 32 || t1 > t0 + 32) {
+            const uint32_t q = atomicAdd(&qn, 1u);
+            qk0[q] = k0, qk1[q] = k1, qt0[q] = t0, qt1[q] = t1, qb[q] = b;
+        } else {
+            for (uint32_t k = k0; k < k1; ++k) owner[k] = b;
+            for (uint32_t t = t0; t < t1; ++t) first[t] = b;
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < qn; ++q) {
+        const uint32_t qv = qb[q];
+        for (uint32_t k = qk0[q] + threadIdx.x; k < qk1[q]; k += blockDim.x) owner[k] = qv;
+        for (uint32_t t = qt0[q] + threadIdx.x; t < qt1[q]; t += blockDim.x) first[t] = qv;
+    }
     if (b >= m) return;
-    const uint32_t k0 = cloc[b] + blk_pre[b >> cs];
-    const uint32_t k1 = b + 1 < m ? cloc[b + 1] + blk_pre[(b + 1) >> cs] : blk_pre[(m + (1u << cs) - 1) >> cs];
-    chunk_off[b] = k0;
-    if (b + 1 == m) chunk_off[m] = k1;
-    for (uint32_t k = k0; k < k1; ++k) owner[k] = b;
-    const uint32_t o = offsets[b], e = offsets[b + 1];
-    for (uint32_t t = (o + L - 1) / L; t * L < e; ++t) first[t] = b;
     const uint32_t c = nchunks[b];
     if (c <= SMALL_MAX) {
         perm[atomicAdd(&cur[c], 1u)] = b;

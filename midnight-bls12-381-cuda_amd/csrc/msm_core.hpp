@@ -286,99 +286,6 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
 }
 
 // ------------------------------------------------------------------------------------
-// 5. bucket sums from chunk partials.  Light buckets (<= SMALL_MAX partials -- every bucket of
-//    random inputs): one thread each.  Heavy buckets (equal scalars, adversarial inputs): cut into
-//    slices of HEAVY_SLICE partials, listed by k_chunk_owner (HeavyTab); one workgroup per slice
-//    sums its slice (strided chains + an LDS tree), and the workgroup that finishes a bucket's
-//    last slice (a counter per bucket: last-block-done) sums the bucket's slice sums.  The slice
-//    workgroups ride in the same launch as the light buckets (HEAVY_BLOCKS extra workgroups that
-//    exit at once when there is no heavy bucket): no extra launch, no side stream, no event.
-// ------------------------------------------------------------------------------------
-static constexpr uint32_t HEAVY_SLICE = 2048;  // chunk partials per heavy slice (one workgroup)
-static constexpr uint32_t HEAVY_BLOCKS = 256;  // workgroups appended to k_bucket_small
-
-// one workgroup's chains hold partial sums: LDS tree, the total ends in chain 0
-template <class L>
-MBLS_DEV Jacobian<L> block_tree(Jacobian<L> acc, uint8_t* sh, uint32_t j, uint32_t chains) {
-    store_jac<L>(sh, j, acc);
-    __syncthreads();
-    for (uint32_t s = chains / 2; s > 0; s >>= 1) {
-        if (j < s) {
-            acc = jac_add(acc, load_jac<L>(sh, j + s));
-            store_jac<L>(sh, j, acc);
-        }
-        __syncthreads();
-    }
-    return acc;
-}
-
-template <class F>
-MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ partials,
-                           uint8_t* __restrict__ buckets, const HeavyTab& H, uint32_t hb, uint32_t nhb) {
-    using L = typename LaneOf<F>::type;
-    constexpr uint32_t LN = LaneOf<F>::LANES;
-    constexpr uint32_t CHAINS = 256 / LN;
-    __shared__ __attribute__((aligned(16))) uint8_t sh[CHAINS * 3 * sizeof(F)];
-    __shared__ uint32_t last;
-    const uint32_t nsl = H.cnt[1];
-    const uint32_t j = threadIdx.x / LN;
-    for (uint32_t g = hb; g < nsl; g += nhb) {
-        const uint32_t e = H.owner[g], b = H.bucket[e];
-        const uint32_t c0 = chunk_off[b] + (g - H.first[e]) * HEAVY_SLICE;
-        const uint32_t c1 = min(c0 + HEAVY_SLICE, chunk_off[b + 1]);
-        Jacobian<L> acc = Jacobian<L>::inf();
-        for (uint32_t k = c0 + j; k < c1; k += CHAINS) acc = jac_add(acc, load_jac<L>(partials, k));
-        acc = block_tree<L>(acc, sh, j, CHAINS);
-        if (j == 0) store_jac<L>(H.res, g, acc);
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0) last = atomicAdd(&H.done[e], 1u) + 1 == H.nslices[e] ? 1u : 0u;
-        __syncthreads();
-        if (last) {  // this workgroup finished bucket b's last slice: sum the slice sums
-            __threadfence();
-            const uint32_t ns = H.nslices[e], f0 = H.first[e];
-            Jacobian<L> tot = Jacobian<L>::inf();
-            for (uint32_t k = j; k < ns; k += CHAINS) tot = jac_add(tot, load_jac<L>(H.res, f0 + k));
-            tot = block_tree<L>(tot, sh, j, CHAINS);
-            if (j == 0) store_jac<L>(buckets, b, tot);
-        }
-        __syncthreads();  // sh and `last` are reused by the next slice
-    }
-}
-
-// light buckets: one thread per bucket (<= SMALL_MAX chunks) sums its chunk partials; thread t
-// takes perm[start + t] (k_chunk_owner: buckets grouped by chunk count, heaviest first, so a
-// wave's lanes run the same number of additions).  Workgroups from `light_blocks` on take the
-// heavy slices.
-template <class F>
-// 2 waves per SIMD: G1 fits anyway (181 VGPRs); G2's pair-sliced sums took 260 VGPRs + 4 AGPRs,
-// i.e. one latency-bound wave per SIMD -- capped at 256 (4 spilled) its bucket sums take 0.93
-// instead of 1.17 ms at 2^20 (A/B x2 on one box, profiles/r04/bs_minw_ab.txt)
-#ifndef MBLS_BS_MINW
-#define MBLS_BS_MINW 2
-#endif
-__global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32_t* __restrict__ chunk_off,
-                                                      const uint32_t* __restrict__ perm, const uint32_t* __restrict__ binbase,
-                                                      uint32_t gwords, const uint8_t* __restrict__ partials,
-                                                      uint8_t* __restrict__ buckets, uint32_t light_blocks, HeavyTab H) {
-    MBLS_TAIL_PRIO();
-    using L = typename LaneOf<F>::type;
-    if (blockIdx.x >= light_blocks) {
-        heavy_slices<F>(chunk_off, partials, buckets, H, blockIdx.x - light_blocks, gridDim.x - light_blocks);
-        return;
-    }
-    const uint32_t start = binbase[0], stop = binbase[gwords];
-    const uint32_t t = start + (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
-    if (t >= stop) return;
-    const uint32_t b = perm[t];
-    const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
-    Jacobian<L> acc = Jacobian<L>::inf();
-    if (k1 > k0) acc = load_jac<L>(partials, k0);
-    for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<L>(partials, k));
-    store_jac<L>(buckets, b, acc);
-}
-
-// ------------------------------------------------------------------------------------
 // Serial phases run on ROW-SLICED arithmetic (mbls_rowfield.hpp): one logical thread =
 // one 16-lane row holding a field element limb-per-lane, so a serial chain of additions
 // costs ~150 instead of ~1.3 K dependent instructions per product.  `rid` = row index.
@@ -448,6 +355,121 @@ struct RedIO<F, MODE_WAVE> {
 };
 template <int MODE>
 constexpr uint32_t lanes_per_chain() { return MODE == MODE_LANE ? 1u : MODE == MODE_ROW ? 16u : 64u; }
+
+// ------------------------------------------------------------------------------------
+// 5. bucket sums from chunk partials.  Light buckets (<= SMALL_MAX partials -- every bucket of
+//    random inputs): one thread each.  Heavy buckets (equal scalars, adversarial inputs): cut into
+//    slices of HEAVY_SLICE partials, listed by k_chunk_owner (HeavyTab); one workgroup per slice
+//    sums its slice (strided chains + an LDS tree), and the workgroup that finishes a bucket's
+//    last slice (a counter per bucket: last-block-done) sums the bucket's slice sums.  The slice
+//    workgroups ride in the same launch as the light buckets (HEAVY_BLOCKS extra workgroups that
+//    exit at once when there is no heavy bucket): no extra launch, no side stream, no event.
+// ------------------------------------------------------------------------------------
+static constexpr uint32_t HEAVY_SLICE = 2048;  // chunk partials per heavy slice (one workgroup)
+static constexpr uint32_t HEAVY_BLOCKS = 512;  // workgroups appended to k_bucket_small (two per CU)
+
+// Heavy buckets: a slice workgroup's lanes sum strided chains of its partials (lane arithmetic:
+// throughput), then its 16 rows sum the chain results ROW-SLICED (RedIO<MODE_ROW>: one 16-lane
+// row per chain, ~5 us per Jacobian addition against ~25 us for a lone lane at one wave per SIMD)
+// and a 4-level row tree through LDS finishes; the slice sums of a bucket are added the same way
+// by the workgroup that finishes its last slice.  The former 8-level lane tree per slice took
+// 0.58 ms for one bucket of 2^16 partials (G1 2^20, every scalar 1) and 1.44 ms for 16.
+template <class F>
+MBLS_DEV RJac<F> row_tree(RJac<F> acc, uint8_t* sh, uint32_t r) {
+    using IO = RedIO<F, MODE_ROW>;
+    constexpr uint32_t ROWS = 256 / 16;
+    IO::st(sh, r, acc);
+    __syncthreads();
+    for (uint32_t s = ROWS / 2; s > 0; s >>= 1) {
+        if (r < s) {
+            acc = IO::add(acc, IO::ld(sh, r + s));
+            IO::st(sh, r, acc);
+        }
+        __syncthreads();
+    }
+    return acc;
+}
+
+// sum of the CHAINS Jacobian points in sh (lane layout), by rows; result in row 0
+template <class F>
+MBLS_DEV RJac<F> rows_sum_chains(uint8_t* sh, uint32_t chains) {
+    using IO = RedIO<F, MODE_ROW>;
+    constexpr uint32_t ROWS = 256 / 16;
+    const uint32_t r = threadIdx.x >> 4;
+    RJac<F> acc = RJac<F>::inf();
+    for (uint32_t k = r; k < chains; k += ROWS) acc = IO::add(acc, IO::ld(sh, k));
+    // row r has read its slots (k = r, r + 16, ...); row_tree overwrites only slot r < 16
+    return row_tree<F>(acc, sh, r);
+}
+
+template <class F>
+MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ partials,
+                           uint8_t* __restrict__ buckets, const HeavyTab& H, uint32_t hb, uint32_t nhb) {
+    using L = typename LaneOf<F>::type;
+    using IO = RedIO<F, MODE_ROW>;
+    constexpr uint32_t LN = LaneOf<F>::LANES;
+    constexpr uint32_t CHAINS = 256 / LN;
+    __shared__ __attribute__((aligned(16))) uint8_t sh[CHAINS * 3 * sizeof(F)];
+    __shared__ uint32_t last;
+    const uint32_t nsl = H.cnt[1];
+    const uint32_t j = threadIdx.x / LN;
+    for (uint32_t g = hb; g < nsl; g += nhb) {
+        const uint32_t e = H.owner[g], b = H.bucket[e];
+        const uint32_t c0 = chunk_off[b] + (g - H.first[e]) * HEAVY_SLICE;
+        const uint32_t c1 = min(c0 + HEAVY_SLICE, chunk_off[b + 1]);
+        Jacobian<L> acc = Jacobian<L>::inf();
+        for (uint32_t k = c0 + j; k < c1; k += CHAINS) acc = jac_add(acc, load_jac<L>(partials, k));
+        store_jac<L>(sh, j, acc);
+        __syncthreads();
+        const RJac<F> ssum = rows_sum_chains<F>(sh, CHAINS);
+        if (threadIdx.x < 16) IO::st(H.res, g, ssum);
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) last = atomicAdd(&H.done[e], 1u) + 1 == H.nslices[e] ? 1u : 0u;
+        __syncthreads();
+        if (last) {  // this workgroup finished bucket b's last slice: sum the slice sums
+            __threadfence();
+            const uint32_t ns = H.nslices[e], f0 = H.first[e], r = threadIdx.x >> 4;
+            RJac<F> tot = RJac<F>::inf();
+            for (uint32_t k = r; k < ns; k += 16) tot = IO::add(tot, IO::ld(H.res, f0 + k));
+            tot = row_tree<F>(tot, sh, r);
+            if (threadIdx.x < 16) IO::st(buckets, b, tot);
+        }
+        __syncthreads();  // sh and `last` are reused by the next slice
+    }
+}
+
+// light buckets: one thread per bucket (<= SMALL_MAX chunks) sums its chunk partials; thread t
+// takes perm[start + t] (k_chunk_owner: buckets grouped by chunk count, heaviest first, so a
+// wave's lanes run the same number of additions).  Workgroups from `light_blocks` on take the
+// heavy slices.
+template <class F>
+// 2 waves per SIMD: G1 fits anyway (181 VGPRs); G2's pair-sliced sums took 260 VGPRs + 4 AGPRs,
+// i.e. one latency-bound wave per SIMD -- capped at 256 (4 spilled) its bucket sums take 0.93
+// instead of 1.17 ms at 2^20 (A/B x2 on one box, profiles/r04/bs_minw_ab.txt)
+#ifndef MBLS_BS_MINW
+#define MBLS_BS_MINW 2
+#endif
+__global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32_t* __restrict__ chunk_off,
+                                                      const uint32_t* __restrict__ perm, const uint32_t* __restrict__ binbase,
+                                                      uint32_t gwords, const uint8_t* __restrict__ partials,
+                                                      uint8_t* __restrict__ buckets, uint32_t light_blocks, HeavyTab H) {
+    MBLS_TAIL_PRIO();
+    using L = typename LaneOf<F>::type;
+    if (blockIdx.x >= light_blocks) {
+        heavy_slices<F>(chunk_off, partials, buckets, H, blockIdx.x - light_blocks, gridDim.x - light_blocks);
+        return;
+    }
+    const uint32_t start = binbase[0], stop = binbase[gwords];
+    const uint32_t t = start + (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
+    if (t >= stop) return;
+    const uint32_t b = perm[t];
+    const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
+    Jacobian<L> acc = Jacobian<L>::inf();
+    if (k1 > k0) acc = load_jac<L>(partials, k0);
+    for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<L>(partials, k));
+    store_jac<L>(buckets, b, acc);
+}
 
 // Scaled running-sum level: every level's outputs carry weight 1, so
 // the last level's single output per window IS the window sum -- no per-level T tree sums on side

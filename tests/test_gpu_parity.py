@@ -720,3 +720,38 @@ def test_msm_g1_2_24_single_and_sharded(amd, gh):
     assert single == ref
     assert sharded == ref
     assert multi == ref
+
+
+def _skewed(case, n, g):
+    """prover-shaped scalar columns: selector-like 0 / 1, small values, one set bit, one repeated
+    value (tools/skew_probe.py times them)"""
+    if case == "ones":
+        return [1] * n
+    if case == "half_one":
+        return [1 if i % 2 == 0 else g.randrange(pr.R) for i in range(n)]
+    if case == "bits8":
+        return [g.randrange(256) for _ in range(n)]
+    if case == "bit_of_64":
+        return [1 << (i % 63) for i in range(n)]
+    if case == "repeated":
+        return [g.randrange(pr.R)] * n
+    raise ValueError(case)
+
+
+@pytest.mark.parametrize("group,log_n,case", [("g1", 15, "ones"), ("g1", 15, "half_one"), ("g1", 15, "bits8"),
+                                              ("g1", 15, "bit_of_64"), ("g1", 15, "repeated"), ("g1", 20, "ones"),
+                                              ("g1", 20, "half_one"), ("g2", 14, "ones"), ("g2", 14, "bits8"),
+                                              ("g2", 14, "repeated")])
+def test_msm_skewed_scalars(amd, gh, group, log_n, case):
+    """skewed scalar distributions put most contributions into a few buckets (heavy parts of the
+    partitioned sort, long owner ranges, heavy bucket slices) -- equal to the oracle"""
+    import torch
+    n = 1 << log_n
+    w = 12 if group == "g1" else 24
+    sc = H.ints_to_limbs(_skewed(case, n, pr.rng(77)), 4)
+    b = torch.zeros((n, w), dtype=torch.int64, device="cuda")
+    amd.gen_bases(group, b, 0x5EED0F20 + log_n)
+    out = amd.msm(group, amd.torch_u64(sc), b, icicle=True, n=n)
+    ref = H.oracle_msm(group, sc, amd.to_numpy_u64(b), threads=16)
+    dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
+    assert gh.decode_icicle(group, out[0]) == dec(ref)
