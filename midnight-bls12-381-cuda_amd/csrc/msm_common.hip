@@ -1358,19 +1358,30 @@ static constexpr uint32_t PS_RS = 8, PS_RK = 6;
 #endif
 static constexpr bool PS_KEEP = MBLS_PS_KEEP != 0;
 
-// rank of this lane's entry in LDS counter cnt[key]: one atomic per wave when its active lanes
-// share the key (skewed scalars: a heavy part's entries all in one fine bucket, whose per-lane
-// atomics serialised -- G1 2^20 with every scalar 1: k_part_sort 2.1 ms), else one per lane.
-// Ranks inside a bucket follow lane order, which only permutes the bucket's summands.
+// rank of this lane's entry in LDS counter cnt[key]: the lanes sharing the key of the first
+// remaining lane take one atomic together (up to PEEL such keys per call), the rest one atomic
+// per lane.  Skewed scalars put most of a heavy part's entries into one fine bucket.  Ranks
+// inside a bucket follow lane order, which only permutes the bucket's summands.  PEEL = 1 / 2 /
+// 4 measured equal within noise on the skewed distributions of tools/skew_probe.py (1 best:
+// half ones 3.53 / 3.63 / 3.65 ms): the heavy part's lone workgroup is not bound by its atomics.
+#ifndef MBLS_PS_PEEL
+#define MBLS_PS_PEEL 1
+#endif
+template <int PEEL>
 MBLS_DEV uint32_t lds_rank(uint32_t* cnt, uint32_t key) {
-    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
-    const uint64_t act = __ballot(1);
-    if (__ballot(key == k0) == act) {
-        const uint32_t leader = (uint32_t)__builtin_ctzll(act);
+    const uint32_t lane = __lane_id();
+    const uint64_t below = (1ull << lane) - 1;
+    uint64_t rem = __ballot(1);
+    for (int p = 0; p < PEEL; ++p) {
+        const uint32_t src = (uint32_t)__builtin_ctzll(rem);
+        const uint32_t k = __shfl(key, (int)src, 64);
+        const uint64_t m = __ballot(key == k) & rem;
         uint32_t base = 0;
-        if (__lane_id() == leader) base = atomicAdd(&cnt[k0], (uint32_t)__popcll(act));
-        base = __shfl(base, leader, 64);
-        return base + (uint32_t)__popcll(act & ((1ull << __lane_id()) - 1));
+        if (lane == src) base = atomicAdd(&cnt[k], (uint32_t)__popcll(m));
+        base = __shfl(base, (int)src, 64);
+        if ((m >> lane) & 1) return base + (uint32_t)__popcll(m & below);
+        rem &= ~m;
+        if (!rem) break;
     }
     return atomicAdd(&cnt[key], 1u);
 }
@@ -1461,7 +1472,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_sort(const uint32_t* __rest
             const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
             const uint32_t k = seg_cnt[seg * NP + part];
             const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
-            part_walk<PACK>(ent, o, k, tl, FB, [&](uint32_t fine, uint32_t) { lds_rank(cnt, fine); });
+            part_walk<PACK>(ent, o, k, tl, FB, [&](uint32_t fine, uint32_t) { lds_rank<MBLS_PS_PEEL>(cnt, fine); });
         }
     }
     // this part's base: the sum of the part totals before it (blockIdx = wl * NP + part, the
@@ -1545,7 +1556,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_sort(const uint32_t* __rest
     const uint32_t span = span_sh;
     const bool staged = span <= PS_STAGE;
     auto place = [&](uint32_t fine, uint32_t val) {
-        const uint32_t pos = pre[fine] + lds_rank(cnt, fine);
+        const uint32_t pos = pre[fine] + lds_rank<MBLS_PS_PEEL>(cnt, fine);
         if (staged)
             ps_stage[pos] = val;
         else
