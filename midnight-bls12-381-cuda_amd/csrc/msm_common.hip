@@ -1555,13 +1555,15 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_sort(const uint32_t* __rest
     // bucket skew) takes the direct stores
     const uint32_t span = span_sh;
     const bool staged = span <= PS_STAGE;
-    auto place = [&](uint32_t fine, uint32_t val) {
-        const uint32_t pos = pre[fine] + lds_rank<MBLS_PS_PEEL>(cnt, fine);
+    // register-kept parts are light (<= PS_RK * PS_TEAM entries per segment): plain atomics
+    auto put = [&](uint32_t pos, uint32_t val) {
         if (staged)
             ps_stage[pos] = val;
         else
             sorted[base + pos] = val;
     };
+    auto place = [&](uint32_t fine, uint32_t val) { put(pre[fine] + lds_rank<MBLS_PS_PEEL>(cnt, fine), val); };
+    auto place_light = [&](uint32_t fine, uint32_t val) { put(pre[fine] + atomicAdd(&cnt[fine], 1u), val); };
     if (keep) {
         const uint32_t vmask = FB ? (1u << (32 - FB)) - 1 : ~0u;
 #pragma unroll
@@ -1570,7 +1572,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_sort(const uint32_t* __rest
             for (uint32_t q = 0; q < PS_RK; ++q)
                 if (tl + q * PS_TEAM < sk[j]) {
                     const uint32_t x = e[j * PS_RK + q];
-                    place(FB ? x >> (32 - FB) : 0u, x & vmask);
+                    place_light(FB ? x >> (32 - FB) : 0u, x & vmask);
                 }
     } else {
         for (uint32_t s = team; s < S; s += nteams) {
