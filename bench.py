@@ -488,6 +488,28 @@ def msm_variants(args, amd, torch, dev, stream, scalars, bases, n, timed, max_ov
                               "results_equal": bool(torch.equal(r2[0], res) and torch.equal(r2[1], res)),
                               "note": "the same 2^20 MSM issued alternately on two caller streams (async, device "
                                       "result), as an async prover issues independent commitments; never `value`"}
+    # skewed scalar columns (selector-like 0 / 1, small values): the heavy-bucket paths
+    # (DESIGN.md section 5 "Skewed scalars"; parity in tests/test_gpu_parity.py::test_msm_skewed_scalars)
+    sk = torch.zeros_like(scalars)
+    amd.gen_scalars(sk, 0x5EED0003, montgomery=False, stream=stream)
+    torch.cuda.synchronize(dev)
+    even = torch.arange(n, device=dev) % 2 == 0
+    skew = {}
+    for name in ("half_one", "bits8", "ones"):
+        if name == "half_one":
+            sk[even] = torch.tensor([1, 0, 0, 0], dtype=torch.int64, device=dev)
+        elif name == "bits8":
+            sk[:, 1:] = 0
+            sk[:, 0] = torch.randint(0, 256, (n,), device=dev, generator=torch.Generator(dev).manual_seed(8))
+        else:
+            sk[:] = torch.tensor([1, 0, 0, 0], dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
+        sk_ms = max_over_ranks(timed(lambda: amd.msm("g1", sk, bases, icicle=True, scalars_mont=False, out=res,
+                                                     stream=stream, is_async=True, n=n), reps))
+        skew[f"{name}_ms"] = round(sk_ms, 4)
+    out["msm_skewed_scalars"] = dict(skew, note="G1 2^20, standard-form scalars: half the scalars 1 (the rest "
+                                     "random), 8-bit scalars, every scalar 1; never `value`")
+    del sk
     # batched MSMs (ICICLE batch_size, shared device bases): members pipelined on two streams
     if args.msm_batch > 1:
         B = args.msm_batch
