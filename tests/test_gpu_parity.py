@@ -740,7 +740,8 @@ def _skewed(case, n, g):
 
 @pytest.mark.parametrize("group,log_n,case", [("g1", 15, "ones"), ("g1", 15, "half_one"), ("g1", 15, "bits8"),
                                               ("g1", 15, "bit_of_64"), ("g1", 15, "repeated"), ("g1", 20, "ones"),
-                                              ("g1", 20, "half_one"), ("g2", 14, "ones"), ("g2", 14, "bits8"),
+                                              ("g1", 20, "half_one"), ("g1", 22, "ones"), ("g2", 14, "ones"),
+                                              ("g2", 14, "bits8"),
                                               ("g2", 14, "repeated")])
 def test_msm_skewed_scalars(amd, gh, group, log_n, case):
     """skewed scalar distributions put most contributions into a few buckets (heavy parts of the
