@@ -365,7 +365,10 @@ constexpr uint32_t lanes_per_chain() { return MODE == MODE_LANE ? 1u : MODE == M
 //    workgroups ride in the same launch as the light buckets (HEAVY_BLOCKS extra workgroups that
 //    exit at once when there is no heavy bucket): no extra launch, no side stream, no event.
 // ------------------------------------------------------------------------------------
-static constexpr uint32_t HEAVY_SLICE = 2048;  // chunk partials per heavy slice (one workgroup)
+#ifndef MBLS_HEAVY_SLICE
+#define MBLS_HEAVY_SLICE 2048
+#endif
+static constexpr uint32_t HEAVY_SLICE = MBLS_HEAVY_SLICE;  // chunk partials per heavy slice (one workgroup)
 static constexpr uint32_t HEAVY_BLOCKS = 512;  // workgroups appended to k_bucket_small (two per CU)
 
 // Heavy buckets: a slice workgroup's lanes sum strided chains of its partials (lane arithmetic:
