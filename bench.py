@@ -119,8 +119,45 @@ def digest(t):
     return hashlib.sha256(t.detach().cpu().numpy().view(np.uint64).tobytes()).hexdigest()[:16]
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`--gpus N` is authoritative.  Without a launcher (no WORLD_SIZE) and N > 1, start
+    torch.distributed.run with N ranks as a CHILD process (never exec: nothing here has touched
+    the GPU, and the child must not replace this process), let rank 0's JSON line through, and
+    return the child's exit code.  Returns None when this process is a rank itself."""
+    env_world = os.environ.get("WORLD_SIZE")
+    same_dev = os.environ.get("MBLS_BENCH_SAME_DEVICE") == "1"
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            sys.stderr.write(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} "
+                             f"ranks; refusing to print a line for a run that was not asked for\n")
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import torch  # device_count() does not initialise the GPU on this image
+    have = torch.cuda.device_count()
+    if have < args.gpus and not same_dev:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {have}; "
+                         f"(rehearsal on one GPU: MBLS_BENCH_SAME_DEVICE=1 MBLS_BENCH_BACKEND=gloo)\n")
+        return 2
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     import torch
     import torch.distributed as dist
     import bls12_381_amd as amd
@@ -132,9 +169,13 @@ def main():
     # rehearsal of the multi-rank path on a one-GPU box (never the driver's runs):
     # MBLS_BENCH_SAME_DEVICE=1 puts every rank on GPU 0, MBLS_BENCH_BACKEND=gloo replaces RCCL
     # (which refuses two ranks on one device); the digests must match the N = 1 run
-    if os.environ.get("MBLS_BENCH_SAME_DEVICE") == "1":
+    same_dev = os.environ.get("MBLS_BENCH_SAME_DEVICE") == "1"
+    if same_dev:
         local = 0
     backend = os.environ.get("MBLS_BENCH_BACKEND", "nccl")
+    if world > 1 and not same_dev and torch.cuda.device_count() < world:
+        sys.stderr.write(f"bench.py: rank {rank}: WORLD_SIZE={world} but {torch.cuda.device_count()} GPUs visible\n")
+        sys.exit(2)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -144,6 +185,14 @@ def main():
             dist.init_process_group(backend)
     amd.lib()
     stream = torch.cuda.current_stream(dev)
+    # which device every rank ran on (the line proves the N it claims)
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "device": local, "uuid": str(getattr(props, "uuid", "")), "name": props.name}
+    ranks_devices = [me]
+    if world > 1:
+        ranks_devices = [None] * world
+        dist.all_gather_object(ranks_devices, me)
+    dist_world = dist.get_world_size() if world > 1 else 1
 
     def barrier_sync():
         torch.cuda.synchronize(dev)
@@ -327,6 +376,9 @@ def main():
             "value": round(msm_per_sec, 3),
             "unit": "MSM/s",
             "n_gpus": world,
+            "world_size": dist_world,
+            "rank_devices": ranks_devices,
+            "same_device_rehearsal": same_dev and world > 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),

@@ -227,9 +227,29 @@ const void* pinned_host_device_pointer(const void* p) {
         return nullptr;
     }
     if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+    // only the alias of the calling device: whether a registered / non-portable allocation's
+    // alias is valid on another device is not something the multi-device shards rely on (they
+    // stage instead)
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || a.device != cur) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
     // the attribute describes the allocation: offset the device alias like the host pointer
     const char* hbase = static_cast<const char*>(a.hostPointer ? a.hostPointer : p);
     return static_cast<const char*>(a.devicePointer) + (static_cast<const char*>(p) - hbase);
+}
+
+size_t device_bytes_from(const void* p) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (!p || hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess || !base) {
+        (void)hipGetLastError();
+        return SIZE_MAX;
+    }
+    const char* b = static_cast<const char*>(base);
+    const char* q = static_cast<const char*>(p);
+    return q >= b && q <= b + size ? (size_t)(b + size - q) : SIZE_MAX;
 }
 
 bool is_device_pointer(const void* p) {

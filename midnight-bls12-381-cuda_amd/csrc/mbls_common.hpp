@@ -113,6 +113,9 @@ bool is_device_pointer(const void* p);
 // device-visible alias of page-locked (pinned / registered) host memory, or nullptr for pageable
 // host memory and device memory
 const void* pinned_host_device_pointer(const void* p);
+// bytes from `p` to the end of the device allocation holding it (hipMemGetAddressRange), or
+// SIZE_MAX when the runtime cannot tell (host memory, foreign allocators)
+size_t device_bytes_from(const void* p);
 
 // Stage profiler: when enabled (mbls_profile_enable / MBLS_PROFILE=1) a ProfScope records a
 // hipEvent pair on the stream around the enclosed launches; mbls_profile_read() sums the

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <map>
+#include <set>
 
 #include "msm_core.hpp"
 
@@ -289,6 +290,33 @@ MBLS_DEV void window_span(int j, int c, int Wg, int sF, int& pos, int& wid) {
 }
 
 // ------------------------------------------------------------------------------------
+// 0. scalars.  The reference's raw entry digitises all 256 bits of a standard-form scalar
+//    (msm_kernels.cu:86-142, W = ceil(256 / c) at :648), so ANY 32-byte s gives s P; on the
+//    order-r subgroup that is (s mod r) P.  The GLV / psi splits and the closed-form digits
+//    assume s < r, so standard scalars are reduced first: 2^256 < 3r, two conditional
+//    subtractions (tests/test_gpu_parity.py::test_msm_noncanonical_scalars).
+//    Montgomery scalars need none: from_mont of any 256-bit word string is already < r.
+// ------------------------------------------------------------------------------------
+MBLS_DEV void reduce_scalar_words(uint32_t (&x)[8]) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        uint32_t t[8];
+        const uint32_t borrow = sub_mod_raw<FrCfg>(t, x);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = borrow ? x[i] : t[i];
+    }
+}
+template <bool MONT>
+MBLS_DEV Fr load_scalar(const uint8_t* __restrict__ scalars, size_t i) {
+    Fr s = load<FrCfg>(scalars + 32 * i);
+    if (MONT)
+        s = from_mont(s);
+    else
+        reduce_scalar_words(s.v);
+    return s;
+}
+
+// ------------------------------------------------------------------------------------
 // 1. digits: one thread per scalar
 // ------------------------------------------------------------------------------------
 template <bool MONT>
@@ -297,8 +325,7 @@ __global__ __launch_bounds__(256) void k_digits(const uint8_t* __restrict__ scal
                                                 uint32_t* __restrict__ ranks, uint32_t* __restrict__ counts) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
-    if (MONT) s = from_mont(s);
+    Fr s = load_scalar<MONT>(scalars, i);
     uint32_t carry = 0;
     for (int w = 0; w < W; ++w) {
         int bit, wid;
@@ -463,8 +490,7 @@ __global__ __launch_bounds__(256) void k_digits_glv(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ counts, SplitLayout lay) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
-    if (MONT) s = from_mont(s);
+    Fr s = load_scalar<MONT>(scalars, i);
     uint32_t m[2][4];
     bool neg[2];
     glv_split(s, m[0], neg[0], m[1], neg[1]);
@@ -596,8 +622,7 @@ MBLS_DEV uint64_t divmod_x(uint32_t (&t)[8]) {
 template <bool MONT>
 MBLS_DEV void psi_split_one(const uint8_t* __restrict__ scalars, uint32_t n, uint4* __restrict__ out, uint32_t i,
                             SplitLayout lay) {
-    Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
-    if (MONT) s = from_mont(s);
+    Fr s = load_scalar<MONT>(scalars, i);
     uint32_t t[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) t[k] = s.v[k];
@@ -813,8 +838,7 @@ __global__ __launch_bounds__(256) void k_glv_split(const uint8_t* __restrict__ s
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     z.run(i, gridDim.x * blockDim.x);
     if (i >= n) return;
-    Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
-    if (MONT) s = from_mont(s);
+    Fr s = load_scalar<MONT>(scalars, i);
     uint32_t m1[4], m2[4];
     bool n1, n2;
     glv_split(s, m1, n1, m2, n2);
@@ -857,8 +881,7 @@ __global__ __launch_bounds__(256) void k_glv_prep(const uint8_t* __restrict__ sc
         block_rows_out<96>(phi_rows + (size_t)b0 * 96, stage, rows);
     }
     if (i >= n) return;
-    Fr s = load<FrCfg>(scalars + 32 * (size_t)i);
-    if (MONT) s = from_mont(s);
+    Fr s = load_scalar<MONT>(scalars, i);
     uint32_t m1[4], m2[4];
     bool n1, n2;
     glv_split(s, m1, n1, m2, n2);
@@ -926,9 +949,11 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_tiled(const uint32_t* __r
                 x[4 * q + 3] = u.w;
             }
             uint32_t negh = 0;
-            if (GLV) {
+            if constexpr (GLV) {
                 negh = x[3] >> 31;
                 x[3] &= 0x7fffffffu;
+            } else {
+                reduce_scalar_words(x);  // standard scalars read in place (section 0)
             }
             const uint32_t d = digit_at<NW>(x, w, c, B, Wg, sF) ^ (negh << 31);
             dig[k] = d;
@@ -1262,9 +1287,11 @@ __global__ __launch_bounds__(DT_THREADS) void k_digits_part(const uint32_t* __re
                 x[4 * q + 3] = u.w;
             }
             uint32_t negh = 0;
-            if (SPLIT) {
+            if constexpr (SPLIT) {
                 negh = x[3] >> 31;
                 x[3] &= 0x7fffffffu;
+            } else {
+                reduce_scalar_words(x);  // standard scalars read in place (section 0)
             }
             const uint32_t d = digit_closed<NW>(x, C, w, c, B, Wg, sF) ^ (negh << 31);
             dig[k] = d;
@@ -1938,6 +1965,32 @@ std::mutex& multi_device_mutex() {
 MultiDevRes*& multi_device_last() {
     static MultiDevRes* last = nullptr;
     return last;
+}
+
+// Peer access between the first device and a shard's device, enabled once per ordered pair
+// (under the multi-device lock): the shard's scalar staging copy reads the first device's
+// memory and the exchange copies the shard's partial back.  Without it hipMemcpyPeerAsync /
+// hipMemcpyDefault between devices may be staged through host memory.  Pairs the hardware
+// cannot map are left to the runtime's staged copy (still correct).
+eIcicleError enable_peer(int from, int to) {
+    static std::set<std::pair<int, int>>* done = new std::set<std::pair<int, int>>();
+    if (from == to || done->count({from, to})) return MBLS_SUCCESS;
+    int can = 0;
+    MBLS_TRY(hipDeviceCanAccessPeer(&can, from, to));
+    if (can) {
+        int cur = 0;
+        MBLS_TRY(hipGetDevice(&cur));
+        MBLS_TRY(hipSetDevice(from));
+        hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+        (void)hipSetDevice(cur);
+        if (e == hipErrorPeerAccessAlreadyEnabled) {
+            (void)hipGetLastError();
+        } else if (e != hipSuccess) {
+            return map_hip_error(e, "hipDeviceEnablePeerAccess");
+        }
+    }
+    done->insert({from, to});
+    return MBLS_SUCCESS;
 }
 
 eIcicleError multi_device_res(int dev, MultiDevRes*& out) {

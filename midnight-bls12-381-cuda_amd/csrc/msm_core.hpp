@@ -1205,6 +1205,22 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     if (msm_size > 0 && (!scalars || !bases)) return MBLS_INVALID_POINTER;
     hipStream_t st = static_cast<hipStream_t>(cfg->stream);
     const int batch = icicle_semantics ? (cfg->batch_size > 0 ? cfg->batch_size : 1) : 1;
+    // The reference's plain device-bases MSMs (core/msm.rs:897-913, 1025-1040, 1097-1110) set
+    // cfg.precompute_factor = MIDNIGHT_GPU_PRECOMPUTE on a buffer of n plain bases; its backend
+    // never reads the factor.  A device allocation too short for n x F table entries cannot be a
+    // precompute_bases table: it runs as factor 1, the reference's result (the
+    // binding should pass PrecomputedBases::factor()).
+    MSMConfig cfg_plain;
+    if (cfg->precompute_factor > 1 && cfg->are_points_on_device && bases && msm_size > 0) {
+        const bool sh = cfg->are_points_shared_in_batch || batch == 1;
+        const size_t want = (size_t)msm_size * (size_t)cfg->precompute_factor * (sh ? 1 : (size_t)batch) *
+                            GroupTraits<F>::AFF;
+        if (device_bytes_from(bases) < want) {
+            cfg_plain = *cfg;
+            cfg_plain.precompute_factor = 1;
+            cfg = &cfg_plain;
+        }
+    }
     MsmPlan P;
     eIcicleError er = make_plan(msm_size > 0 ? msm_size : 1, cfg, P, std::is_same<F, Fq>::value ? 2 : 4);
     if (er != MBLS_SUCCESS) return er;
@@ -1307,6 +1323,10 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     }
     // the side stream runs the tails in member order: its last event covers them all
     if (piped) MBLS_TRY(hipStreamWaitEvent(st, ctx.events[4 + ((batch - 1) & 1)], 0));
+    // every side stream is joined into `st` by now (the table's ev[1] before the accumulation,
+    // the fronts' front_done, the tails' last event above): only an early error return leaves
+    // the lease's fallback join to do
+    ctx.forked = false;
     if (!direct) {
         if (entry == MSM_ICICLE && !piped) {
             hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3((batch + 63) / 64), dim3(64), 0, st, d_r, d_r, batch);
@@ -1342,6 +1362,7 @@ std::mutex& multi_device_mutex();
 // partial / gather slots, whatever streams the two calls use); under the multi-device lock
 MultiDevRes*& multi_device_last();
 eIcicleError multi_device_res(int dev, MultiDevRes*& out);
+eIcicleError enable_peer(int from, int to);
 
 template <class F>
 eIcicleError msm_multi_device(const void* scalars, const void* const* bases_per_dev, const int* devs, int ndev,
@@ -1368,6 +1389,10 @@ eIcicleError msm_multi_device(const void* scalars, const void* const* bases_per_
     MultiDevRes* r0 = nullptr;
     eIcicleError er = multi_device_res(d0, r0);
     if (er != MBLS_SUCCESS) return er;
+    for (int k = 1; k < ndev; ++k) {  // both directions: scalars d0 -> d, the partial d -> d0
+        if ((er = enable_peer(d0, devs[k])) != MBLS_SUCCESS) return er;
+        if ((er = enable_peer(devs[k], d0)) != MBLS_SUCCESS) return er;
+    }
     hipStream_t st0 = cfg->stream ? static_cast<hipStream_t>(cfg->stream) : r0->stream;
     // shard streams are forked from the caller's stream: the caller's earlier work on its
     // inputs (a device scalar upload, say) is ordered before every shard

@@ -391,8 +391,10 @@ static Fr to_dev(const uint64_t* h) {
 }
 
 // (re)build the stage tables of `dom` (the current device's) up to 2^max_log; caller holds
-// g_domain_mu.  A superseded table stays alive while any snapshot of it does (DomainTables)
-static eIcicleError build_domain(Domain& dom, int max_log, hipStream_t st) {
+// g_domain_mu.  A superseded table stays alive while any snapshot of it does (DomainTables);
+// the domain's own reference moves to *old, which the caller drops AFTER releasing the lock
+// (the destructor's device synchronisation must not run under g_domain_mu: ADVICE r4)
+static eIcicleError build_domain(Domain& dom, int max_log, hipStream_t st, std::shared_ptr<DomainTables>& old) {
     if (dom.tables && dom.tables->max_log >= max_log) return MBLS_SUCCESS;
     const int order = dom.order_log;
     if (max_log > order) return MBLS_INVALID_ARGUMENT;
@@ -411,6 +413,7 @@ static eIcicleError build_domain(Domain& dom, int max_log, hipStream_t st) {
     MBLS_TRY(hipGetLastError());
     MBLS_TRY(hipStreamSynchronize(st));
     t->max_log = max_log;
+    old = std::move(dom.tables);
     dom.tables = std::move(t);
     return MBLS_SUCCESS;
 }
@@ -490,13 +493,14 @@ eIcicleError ntt_init_domain(const mbls_fr_t* root, const NTTInitDomainConfig* c
         K = hfr_log_order(m);
     }
     if (K < 0) return MBLS_INVALID_ARGUMENT;
+    std::shared_ptr<DomainTables> old;  // dropped after the lock (declared before it)
     std::lock_guard<std::mutex> lk(g_domain_mu);
     Domain* dom = current_domain();
     if (!dom) return MBLS_INVALID_DEVICE;
     // the tables are canonical (independent of the root): a smaller order only bounds sizes
     dom->order_log = K;
     // stage tables up to 2^22 now (2 x 128 MiB); larger sizes extend them on first use
-    return build_domain(*dom, K < 22 ? K : 22, st);
+    return build_domain(*dom, K < 22 ? K : 22, st, old);
 }
 
 eIcicleError ntt_release_domain() {
@@ -572,6 +576,7 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
     int batch = cfg->batch_size > 0 ? cfg->batch_size : 1;
     hipStream_t st = static_cast<hipStream_t>(cfg->stream);
     std::shared_ptr<DomainTables> tables;  // snapshot: valid for the whole enqueue below
+    std::shared_ptr<DomainTables> superseded;  // an extension's old tables, dropped outside the lock
     {
         std::lock_guard<std::mutex> lk(g_domain_mu);
         Domain* dom = current_domain();
@@ -581,7 +586,7 @@ eIcicleError ntt_call(const mbls_fr_t* input, int size, NTTDir dir, const NTTCon
             // lazily build / extend this device's stage tables (init_domain builds up to 2^22)
             int want = log_n < 20 ? 20 : log_n;
             if (want > dom->order_log) want = dom->order_log;
-            eIcicleError er = build_domain(*dom, want, st);
+            eIcicleError er = build_domain(*dom, want, st, superseded);
             if (er != MBLS_SUCCESS) return er;
         }
         tables = dom->tables;

@@ -3,7 +3,8 @@
 (oracle/pyref.py).  Deterministic: re-running reproduces the committed JSON byte for byte.
 
 Values are stored as hex strings of the integer a byte layout holds:
-  * scalars in MSM fixtures: standard-form integers in [0, r);
+  * scalars in MSM fixtures: standard-form integers in [0, r), except the
+    ``noncanonical_scalars`` case ([r, 2^256): the result is (s mod r) P);
   * points: affine standard-form coordinates, ``null`` = identity
     (G2 coordinates are [c0, c1] pairs);
   * vecops / NTT fixtures: the raw 256-bit value of the limbs, i.e. the Montgomery-encoded
@@ -145,6 +146,16 @@ def _msm_cases(group: str, seed: int, rand_sizes):
     add_case("random_scalars_generator_bases_40", sc, [gen] * 40)
     sc = [g.randrange(1, 64) for _ in range(64)]
     add_case("small_scalars_same_base_64", sc, [P1] * 64)
+    # standard-form scalars >= r: the reference's raw entry digitises all 256
+    # bits (msm_kernels.cu:86-142, :648), i.e. s P = (s mod r) P; own generator, so the cases
+    # above are unchanged
+    g2 = pr.rng(seed ^ 0xB16)
+    R = pr.R
+    sc = [R, R + 1, 2 * R - 1, 2 * R, (1 << 255), (1 << 256) - 1, (1 << 256) - R, R + pr.GLV_LAMBDA,
+          R + (pr.GLV_LAMBDA >> 1) + 1, R + pr.PSI_X ** 3] + [g2.randrange(R, 1 << 256) for _ in range(6)]
+    bs = [mul(pr.random_fr(g2), gen) for _ in range(len(sc))]
+    bs[1] = bs[0]
+    add_case("noncanonical_scalars", sc, bs)
     return cases
 
 

@@ -145,30 +145,31 @@ def test_two_threads_msm_and_ntt_concurrent(amd, gh):
     assert all(np.array_equal(g, ref_ntt) for g in got_ntt)
 
 
-@pytest.mark.parametrize("ndev", [1, 3])
-def test_msm_multi_device_entry(amd, gh, ndev):
-    """mbls_g1_msm_multi_device (the single-process form of SURVEY.md 8e): shards of an uneven
+@pytest.mark.parametrize("group,ndev", [("g1", 1), ("g1", 3), ("g2", 1), ("g2", 3)])
+def test_msm_multi_device_entry(amd, gh, group, ndev):
+    """mbls_g*_msm_multi_device (the single-process form of SURVEY.md 8e): shards of an uneven
     split, each with its own bases buffer, on device 0 (one GPU here: the shards run in turn),
     host and device scalars, host and device result -- equal to the oracle"""
     import torch
-    n = (1 << 18) + 5
+    n = (1 << 18) + 5 if group == "g1" else (1 << 14) + 5
+    w, nl = (12, 18) if group == "g1" else (24, 36)
+    dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
     s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
     amd.gen_scalars(s, 0x5EED0B31, montgomery=True)
-    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
-    amd.gen_bases("g1", b, 0x5EED0B32)
+    b = torch.zeros((n, w), dtype=torch.int64, device="cuda")
+    amd.gen_bases(group, b, 0x5EED0B32)
     torch.cuda.synchronize()
-    ref = H.g1_from_affine_mont(H.oracle_msm("g1", _std_scalars(0x5EED0B31, n), amd.to_numpy_u64(b),
-                                             threads=ORACLE_THREADS))
+    ref = dec(H.oracle_msm(group, _std_scalars(0x5EED0B31, n), amd.to_numpy_u64(b), threads=ORACLE_THREADS))
     shards = [b[n * k // ndev:n * (k + 1) // ndev].clone() for k in range(ndev)]
     torch.cuda.synchronize()
-    r = amd.msm_multi_device("g1", s, shards, [0] * ndev, n)
-    assert gh.decode_icicle("g1", r[0]) == ref
-    out = torch.zeros((1, 18), dtype=torch.int64, device="cuda")
-    amd.msm_multi_device("g1", np.ascontiguousarray(amd.to_numpy_u64(s)), shards, [0] * ndev, n, out=out)
+    r = amd.msm_multi_device(group, s, shards, [0] * ndev, n)
+    assert gh.decode_icicle(group, r[0]) == ref
+    out = torch.zeros((1, nl), dtype=torch.int64, device="cuda")
+    amd.msm_multi_device(group, np.ascontiguousarray(amd.to_numpy_u64(s)), shards, [0] * ndev, n, out=out)
     torch.cuda.synchronize()
-    assert gh.decode_icicle("g1", amd.to_numpy_u64(out)[0]) == ref
+    assert gh.decode_icicle(group, amd.to_numpy_u64(out)[0]) == ref
     with pytest.raises(amd.IcicleError):
-        amd.msm_multi_device("g1", s, shards, [99] * ndev, n)
+        amd.msm_multi_device(group, s, shards, [99] * ndev, n)
 
 
 def test_vector_sum_staged_batch(amd):
@@ -192,3 +193,53 @@ def test_vector_sum_staged_batch(amd):
         assert np.array_equal(got_host[k], acc[0]), k
         assert np.array_equal(got_dev[k], acc[0]), k
     assert amd.scratch_stats()[0] - m0 <= 1  # at most one arena growth, never per call
+
+
+class _RawDev:
+    """a bare hipMalloc'd buffer (the Rust DeviceVec::device_malloc shape) for the binding"""
+    is_cuda = True
+
+    def __init__(self, hip, nbytes):
+        self.hip, self.p = hip, ctypes.c_void_p()
+        hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        hip.hipFree.argtypes = [ctypes.c_void_p]
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        assert hip.hipMalloc(ctypes.byref(self.p), nbytes) == 0
+
+    def data_ptr(self):
+        return self.p.value
+
+    def upload(self, arr):
+        assert self.hip.hipMemcpy(self.p, arr.ctypes.data, arr.nbytes, 1) == 0  # hipMemcpyHostToDevice
+
+    def free(self):
+        self.hip.hipFree(self.p)
+
+
+@pytest.mark.parametrize("group", ["g1", "g2"])
+def test_precompute_factor_on_plain_device_bases(amd, gh, hip, group):
+    """core/msm.rs:897-913 / 1025-1040 / 1097-1110 pass n plain device bases with
+    cfg.precompute_factor = MIDNIGHT_GPU_PRECOMPUTE (4 recommended); the reference backend
+    ignores the factor.  A device allocation too short for an n x F table runs as factor 1
+    (INTEGRATION.md "precompute_factor on plain device bases")"""
+    import torch
+    n, w = 3000, (12 if group == "g1" else 24)
+    b = torch.zeros((n, w), dtype=torch.int64, device="cuda")
+    amd.gen_bases(group, b, 0x5EED0B01)
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0B02, montgomery=True)
+    torch.cuda.synchronize()
+    bn, sn = amd.to_numpy_u64(b), amd.to_numpy_u64(s)
+    raw = _RawDev(hip, bn.nbytes)
+    try:
+        raw.upload(np.ascontiguousarray(bn))
+        ref = amd.msm(group, sn, b, scalars_mont=True, n=n)
+        dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
+        std = np.zeros((n, 4), dtype=np.uint64)
+        H.oracle().orc_gen_scalars(H.ptr(std), 0x5EED0B02, n)
+        assert gh.decode_icicle(group, ref[0]) == dec(H.oracle_msm(group, std, bn, threads=ORACLE_THREADS))
+        for F in (2, 4, 8):
+            r = amd.msm(group, sn, raw, scalars_mont=True, precompute_factor=F, n=n)
+            assert np.array_equal(r, ref), F
+    finally:
+        raw.free()

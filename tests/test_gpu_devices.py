@@ -210,18 +210,22 @@ def test_ntt_replicas_on_two_devices(amd):
 
 
 @pytest.mark.skipif("_ndev() < 2")
-@pytest.mark.parametrize("scalars_on", ["device", "host"])
-def test_msm_multi_device_distinct_devices(amd, gh, scalars_on):
-    """mbls_g1_msm_multi_device over devices [0, 1, ...]: scalars on device 0 (staged to the other
-    shards by peer copies) or on the host, each shard's bases on its own device, partials peer-
-    copied to device 0 -- equal to the oracle"""
+@pytest.mark.parametrize("group", ["g1", "g2"])
+@pytest.mark.parametrize("scalars_on", ["device", "host", "pinned"])
+def test_msm_multi_device_distinct_devices(amd, gh, group, scalars_on):
+    """mbls_g*_msm_multi_device over devices [0, 1, ...]: scalars on device 0 (staged to the other
+    shards by peer copies, peer access enabled by the library), on the host, or in page-locked
+    host memory (read in place only by the device whose alias it is; staged elsewhere), each
+    shard's bases on its own device, partials peer-copied to device 0 -- equal to the oracle"""
     import torch
     ndev = min(_ndev(), 8)
-    n = (1 << 18) + 13
+    n = (1 << 18) + 13 if group == "g1" else (1 << 15) + 13
+    w = 12 if group == "g1" else 24
+    dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
     s = torch.zeros((n, 4), dtype=torch.int64, device="cuda:0")
     amd.gen_scalars(s, 0x5EED0D51, montgomery=True)
-    b0 = torch.zeros((n, 12), dtype=torch.int64, device="cuda:0")
-    amd.gen_bases("g1", b0, 0x5EED0D52)
+    b0 = torch.zeros((n, w), dtype=torch.int64, device="cuda:0")
+    amd.gen_bases(group, b0, 0x5EED0D52)
     torch.cuda.synchronize(0)
     shards = []
     for k in range(ndev):
@@ -229,11 +233,15 @@ def test_msm_multi_device_distinct_devices(amd, gh, scalars_on):
         shards.append(b0[lo:hi].to(f"cuda:{k}"))
     for k in range(ndev):
         torch.cuda.synchronize(k)
-    sc = s if scalars_on == "device" else np.ascontiguousarray(amd.to_numpy_u64(s))
-    r = amd.msm_multi_device("g1", sc, shards, list(range(ndev)), n)
-    ref = H.g1_from_affine_mont(H.oracle_msm("g1", _std_scalars(0x5EED0D51, n), amd.to_numpy_u64(b0),
-                                             threads=ORACLE_THREADS))
-    assert gh.decode_icicle("g1", r[0]) == ref
+    if scalars_on == "device":
+        sc = s
+    elif scalars_on == "host":
+        sc = np.ascontiguousarray(amd.to_numpy_u64(s))
+    else:
+        sc = s.cpu().pin_memory()
+    r = amd.msm_multi_device(group, sc, shards, list(range(ndev)), n)
+    ref = dec(H.oracle_msm(group, _std_scalars(0x5EED0D51, n), amd.to_numpy_u64(b0), threads=ORACLE_THREADS))
+    assert gh.decode_icicle(group, r[0]) == ref
 
 
 @pytest.mark.parametrize("offset", [0, 3])

@@ -594,6 +594,70 @@ def test_msm_psi_split_boundaries(amd, gh):
     assert gh.decode_icicle("g2", r[0]) == ref
 
 
+@pytest.mark.parametrize("group", ["g1", "g2"])
+def test_msm_noncanonical_scalars(amd, gh, group):
+    """Standard-form scalars >= r.  The reference's raw entry digitises all
+    256 bits (msm_kernels.cu:86-142, W = ceil(256 / c) at :648), so any 32-byte s gives s P, and
+    its MSM test plan lists scalars >= the modulus (test_msm_security.cu:48).  Every plan the
+    library has -- GLV / psi split (per-call images and prepared tables), shift tables, the split
+    on slot 0 of a table, c > 16, a batch -- through the raw entry and the ICICLE entry with
+    are_scalars_montgomery_form = false, against the oracle's 256-bit Pippenger (and pyref, which
+    reduces mod r).  Montgomery scalars: any 32-byte word string x stands for x R^-1 mod r."""
+    import torch
+    R = pr.R
+    g = pr.rng(91 if group == "g1" else 92)
+    odd = [R, R + 1, R + 5, 2 * R - 1, 2 * R, 2 * R + 1, (1 << 255), (1 << 255) + 3, (1 << 256) - 1,
+           (1 << 256) - R, (1 << 256) - 2, 3 * R - (1 << 256) + R]
+    odd += [g.randrange(R, 1 << 256) for _ in range(20)]
+    edge = H.glv_edge_scalars() if group == "g1" else H.psi_edge_scalars()
+    sc = odd + [e + R for e in edge if e + R < (1 << 256)] + [g.randrange(R) for _ in range(24)]
+    n = len(sc)
+    w, split = (12, 2) if group == "g1" else (24, 4)
+    b = torch.zeros((n, w), dtype=torch.int64, device="cuda")
+    amd.gen_bases(group, b, 0x5EED0E01 if group == "g1" else 0x5EED0E02)
+    b[1] = b[0]  # equal points: exceptional additions inside a bucket
+    bn = amd.to_numpy_u64(b)
+    s = H.ints_to_limbs(sc, 4)
+    dec = H.g1_from_affine_mont if group == "g1" else H.g2_from_affine_mont
+    ref = dec(H.oracle_msm(group, s, bn))
+    assert ref == dec(H.oracle_msm(group, H.ints_to_limbs([x % R for x in sc], 4), bn))
+    if group == "g1":  # pyref (independent big-integer restatement) on a prefix
+        k = 12
+        pts = [H.g1_from_affine_mont(bn[i]) for i in range(k)]
+        assert dec(H.oracle_msm(group, np.ascontiguousarray(s[:k]), np.ascontiguousarray(bn[:k]))) == \
+            pr.msm_shared_doubling(sc[:k], pts, "g1")
+    for c in (0, 5, 13, 16, 18):
+        r = amd.msm(group, s, bn, c=c, n=n)
+        assert gh.decode_icicle(group, r[0]) == ref, ("icicle", c)
+    r = amd.msm(group, s, bn, icicle=False, n=n)
+    assert gh.decode_jacobian_mont(group, r[0]) == ref, "raw"
+    # device scalars, async on a stream
+    sd = amd.torch_u64(s)
+    out = torch.zeros((1, 18 if group == "g1" else 36), dtype=torch.int64, device="cuda")
+    amd.msm(group, sd, b, out=out, is_async=True, n=n)
+    torch.cuda.synchronize()
+    assert gh.decode_icicle(group, amd.to_numpy_u64(out)[0]) == ref, "device"
+    # prepared table (the split against [P, endo P, ...]), shift tables and slot 0 of a table
+    factors = (split, 3, 4, 8) if group == "g1" else (split, 2, 3, 8)
+    for F in factors:
+        table = amd.precompute_bases(group, b, F, n)
+        for c in (0, 16):
+            r = amd.msm(group, s, table, c=c, precompute_factor=F, n=n)
+            assert gh.decode_icicle(group, r[0]) == ref, ("table", F, c)
+        r = amd.msm(group, s, table, icicle=False, precompute_factor=F, n=n)
+        assert gh.decode_jacobian_mont(group, r[0]) == ref, ("table raw", F)
+    # batch of 2 with shared bases: member 0 the odd scalars, member 1 the same reversed
+    s2 = np.ascontiguousarray(np.concatenate([s, s[::-1]]))
+    r = amd.msm(group, s2, bn, batch=2, n=n)
+    ref1 = dec(H.oracle_msm(group, np.ascontiguousarray(s[::-1]), bn))
+    assert gh.decode_icicle(group, r[0]) == ref and gh.decode_icicle(group, r[1]) == ref1, "batch"
+    # Montgomery-form words >= r: the ICICLE entry converts x -> x R^-1 mod r
+    mont = H.ints_to_limbs(sc, 4)
+    ref_m = dec(H.oracle_msm(group, H.ints_to_limbs([(x * pr.FR_RINV) % R for x in sc], 4), bn))
+    r = amd.msm(group, mont, bn, scalars_mont=True, n=n)
+    assert gh.decode_icicle(group, r[0]) == ref_m, "montgomery"
+
+
 # ----------------------------------------------------------------------------- benchmarked workloads
 # bench.py's inputs exactly (seeds, sizes, entry points, flags), bit-exact against the oracle
 ORACLE_THREADS = 16  # the GPU box's CPU share
