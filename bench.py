@@ -30,20 +30,10 @@ PKG = os.path.join(ROOT, "midnight-bls12-381-cuda_amd")
 sys.path.insert(0, PKG)
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
-MAD_RATE_T = 20.9         # measured v_mad_u64_u32 issue rate, T/s (profiles/r01/microbench.txt)
 MSM_BYTES_PER_POINT = 128  # 32 B scalar + 96 B affine base
 G2_BYTES_PER_POINT = 224   # 32 B scalar + 192 B affine base
 NTT_BYTES_PER_ELEM = 64    # one read + one write of 32 B per transform
 VEC_BYTES_PER_ELEM = 96    # read a, b; write out
-# v_mad_u64_u32 per G1 mixed addition (madd-2007-bl, lazy Y3): 5 Fq products x 288 + 4 squares x
-# 222 + one two-product lazy sum x 432
-MADS_PER_G1_MADD = 5 * 288 + 4 * 222 + 432
-# G2 (pair-sliced Fq2, psi split: 4 streams x 4 windows of 2^20 = 16.8 M mixed additions): one
-# Fq2 product = 2 lanes x one lazy Fq product-sum (432 mads), a square 2 x 288; madd-2007-bl in
-# Fq2 = 7 products + 4 squares
-MADS_PER_G2_MADD = 7 * 2 * 432 + 4 * 2 * 288
-# per Fr butterfly product (FIPS Fr: 64 product mads + 56 reduction mads, r = 1 mod 2^32)
-MADS_PER_FR_MUL = 120
 PROFILES = os.path.join(ROOT, "profiles")
 
 
@@ -75,20 +65,48 @@ def pmc_counter(kernel, counter):
     return (_pmc_kernel(kernel) or {}).get(counter)
 
 
-# VALU issue cost in cycles per wave-instruction: v_mad_u64_u32 (an INT64 instruction) is
-# quarter rate, 8 cycles (profiles/r01/microbench.txt: 34.3 mad/clk/CU); other VALU 2 cycles
-# (MI355X_MICROARCH.md: a wave issues a VALU instruction over 2 cycles)
-MAD_CYCLES, VALU_CYCLES, SIMDS, CLOCK_GHZ = 8, 2, 1024, 2.4
+# VALU issue model, MEASURED (tools/valu_ceiling.hip, profiles/r05/valu_ceiling.json): on gfx950 a
+# wave64 VALU instruction issues over ~4 SIMD cycles whether it is v_mad_u64_u32 (4.4 at the
+# throttled 2.16 GHz a pure-mad loop runs at) or v_add_co / v_addc_co (4.1); the round-1..4 model
+# (8 cycles per INT64 instruction, 2 otherwise, 2.4 GHz) was wrong on both and is gone.
+SIMDS = 1024
 
 
-def valu_issue_bound_ms(kernel):
-    """lower bound on a kernel's duration from its committed VALU instruction counts: every
-    INT64 instruction at the mad cost, the rest at the full rate, all SIMDs busy"""
-    v, i64 = pmc_counter(kernel, "SQ_INSTS_VALU"), pmc_counter(kernel, "SQ_INSTS_VALU_INT64")
-    if v is None or i64 is None:
+def valu_issue_bound_ms(kernel, cyc_per_instr, mhz):
+    """a kernel's VALU issue time from its committed instruction count (all VALU at the measured
+    cycles per wave-instruction, all SIMDs busy, the measured clock)"""
+    v = pmc_counter(kernel, "SQ_INSTS_VALU")
+    if v is None or not cyc_per_instr or not mhz:
         return None
-    cycles = (i64 * MAD_CYCLES + (v - i64) * VALU_CYCLES) / SIMDS
-    return cycles / (CLOCK_GHZ * 1e6)
+    return v * cyc_per_instr / SIMDS / (mhz * 1e3)
+
+
+CEILING_BIN = os.path.join(ROOT, "tools", "valu_ceiling")
+
+
+def valu_ceiling():
+    """Measured VALU ceilings (tools/valu_ceiling.hip): k_accumulate<G1>'s
+    arithmetic (same madd / mmadd code, same 168-VGPR / 3-wave bounds, points from LDS) and
+    k_ntt_pass's radix-4 body, register-resident.  Run live on this box as a child process when
+    the binary is built (build() builds it), else the committed measurement."""
+    import subprocess
+    if os.path.exists(CEILING_BIN):
+        try:
+            out = subprocess.run([CEILING_BIN, "24"], capture_output=True, text=True, timeout=120)
+            if out.returncode == 0:
+                d = json.loads(out.stdout)
+                d["source"] = "live: tools/valu_ceiling 24 on this box"
+                return d
+        except (OSError, ValueError, subprocess.TimeoutExpired):
+            pass
+    path = os.path.join(PROFILES, "r05", "valu_ceiling.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        d["source"] = f"committed: {os.path.relpath(path, ROOT)}"
+        return d
+    except (OSError, ValueError):
+        return None
 
 
 def parse():
@@ -359,17 +377,20 @@ def main():
         # dominant kernel: k_accumulate<G1>; algorithmic bytes = 128 B x points per launch
         msm_ach = MSM_BYTES_PER_POINT * n / (acc_ms * 1e-3) / 1e9 if acc_ms else None
         contributions = 2 * n * ((128 + 16 - 1) // 16)  # GLV: 2n digit streams x 8 windows (c = 16)
-        # mads issued: the committed INT64 counter (v_mad_u64_u32 plus a few 64-bit shifts and
-        # compares) when present, else the algorithmic count (an upper estimate: a chunk's first
-        # point costs no addition and its second the cheaper affine + affine step)
-        i64c = pmc_counter("k_accumulate<G1>", "SQ_INSTS_VALU_INT64")
-        mads_issued = i64c * 64 if i64c else contributions * MADS_PER_G1_MADD
-        mad_t = mads_issued / (acc_ms * 1e-3) / 1e12 if acc_ms else None
         ntt_ach = NTT_BYTES_PER_ELEM * nn / (ntt_ms * 1e-3) / 1e9 if ntt_ms else None
-        ntt_mad_t = (nn // 2) * args.ntt_log * MADS_PER_FR_MUL / (ntt_ms * 1e-3) / 1e12 if ntt_ms else None
         _, pmc_src = pmc_summary()
-        passes = [valu_issue_bound_ms(k) for k in ("k_ntt_pass<true, false, false>", "k_ntt_pass<false, false, false>",
-                                                     "k_ntt_pass<false, true, false>")]
+        ceil = valu_ceiling() or {}
+        acc_c, ntt_c = ceil.get("acc_ceiling") or {}, ceil.get("ntt_ceiling") or {}
+        isa = ceil.get("isa_2") or {}
+        cyc = isa.get("simd_cycles_per_wave_instr")
+        # the ceiling's ns per contribution at this MSM's contribution count
+        acc_ceiling_ms = acc_c["ns_per_contribution_chip"] * contributions * 1e-6 if acc_c else None
+        ntt_ceiling_ms = (ntt_c["ms_per_2^22_transform_10_pairs"] * (args.ntt_log - 2) / 20
+                          if ntt_c and args.ntt_log % 2 == 0 else None)
+        acc_issue = valu_issue_bound_ms("k_accumulate<G1>", cyc, acc_c.get("mhz_med"))
+        passes = [valu_issue_bound_ms(k, cyc, ntt_c.get("mhz_med"))
+                  for k in ("k_ntt_pass<true, false, false>", "k_ntt_pass<false, false, false>",
+                            "k_ntt_pass<false, true, false>")]
         ntt_issue_ms = round(sum(passes), 4) if args.ntt_log == 22 and all(p is not None for p in passes) else None
         out = {
             "metric": "G1 MSM/sec at 2^20 points + Fr NTT/sec at 2^22 (bit-exact vs BLST)",
@@ -404,28 +425,32 @@ def main():
                          "traffic_source": f"{pmc_src} (HBM bytes per launch)" if pmc_src else None,
                          "note": "VALU-bound (v_mad_u64_u32): see roofline_valu"},
             "roofline_valu": {"kernel": "k_accumulate<G1>", "bound": "valu",
-                              "achieved": round(mad_t, 3) if mad_t else None, "peak": MAD_RATE_T,
-                              "unit": "T v_mad_u64_u32/s", "frac": round(mad_t / MAD_RATE_T, 4) if mad_t else None,
-                              "mads_per_launch": round(mads_issued),
-                              "mads_source": "counter (SQ_INSTS_VALU_INT64 x 64)" if i64c else "algorithmic",
-                              "mads_algorithmic_per_launch": contributions * MADS_PER_G1_MADD,
-                              "counter_int64_per_launch": (round(i64 * 64) if (i64 := pmc_counter("k_accumulate<G1>", "SQ_INSTS_VALU_INT64")) else None),
+                              "achieved": round(contributions / (acc_ms * 1e-3) / 1e9, 3) if acc_ms else None,
+                              "peak": round(contributions / (acc_ceiling_ms * 1e-3) / 1e9, 3) if acc_ceiling_ms else None,
+                              "unit": "G mixed additions/s",
+                              "frac": round(acc_ceiling_ms / acc_ms, 4) if acc_ceiling_ms and acc_ms else None,
+                              "ceiling_source": "microbench", "ceiling_ms": round(acc_ceiling_ms, 4) if acc_ceiling_ms else None,
+                              "ceiling": acc_c or None, "ceiling_run": ceil.get("source"),
+                              "measured_cycles_per_valu_instr": cyc,
                               "counter_valu_insts_per_launch": pmc_counter("k_accumulate<G1>", "SQ_INSTS_VALU"),
-                              "counter_issue_bound_ms": (round(b, 4) if (b := valu_issue_bound_ms("k_accumulate<G1>")) else None),
-                              "counter_issue_frac": (round(b / acc_ms, 4) if (b := valu_issue_bound_ms("k_accumulate<G1>")) and acc_ms else None),
-                              "counter_source": f"{pmc_src} (SQ_INSTS_VALU, SQ_INSTS_VALU_INT64 per launch)" if pmc_src else None,
-                              "note": f"achieved = mads issued per launch / kernel time; algorithmic bound "
-                                      f"{contributions} mixed additions x {MADS_PER_G1_MADD} mads; peak = measured "
-                                      "mad issue rate; counter_issue_frac = the "
-                                      "kernel's VALU issue time from its committed instruction counts (INT64 at 8, "
-                                      "other VALU at 2 cycles per wave-instruction, 1024 SIMDs, 2.4 GHz) / its "
-                                      "measured time"},
+                              "counter_issue_ms": round(acc_issue, 4) if acc_issue else None,
+                              "counter_issue_frac": round(acc_issue / acc_ms, 4) if acc_issue and acc_ms else None,
+                              "counter_source": f"{pmc_src} (SQ_INSTS_VALU per launch)" if pmc_src else None,
+                              "note": f"{contributions} mixed additions per launch; peak = k_acc_ceiling "
+                                      "(tools/valu_ceiling.hip: the same madd / mmadd code, launch bounds and chunk "
+                                      "structure with the points in LDS: no random gathers), measured on the box; "
+                                      "frac = ceiling time / kernel time.  counter_issue_ms = the committed VALU "
+                                      "instruction count at the measured cycles per wave-instruction and clock"},
             "roofline_ntt": {"kernel": "k_ntt_pass x passes (one transform)", "bound": "hbm",
-                             "counter_issue_bound_ms": ntt_issue_ms, "counter_issue_frac": (round(ntt_issue_ms / ntt_ms, 4) if ntt_issue_ms and ntt_ms else None),
                              "achieved": round(ntt_ach, 2) if ntt_ach else None, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(ntt_ach / HBM_PEAK_GBS, 5) if ntt_ach else None,
                              "traffic": ntt_traffic(args.ntt_log),
-                             "valu_frac": round(ntt_mad_t / MAD_RATE_T, 4) if ntt_mad_t else None,
+                             "valu_ceiling_ms": round(ntt_ceiling_ms, 4) if ntt_ceiling_ms else None,
+                             "valu_frac": round(ntt_ceiling_ms / ntt_ms, 4) if ntt_ceiling_ms and ntt_ms else None,
+                             "valu_ceiling_source": "microbench (k_ntt_ceiling: the pass's radix-4 body, "
+                                                    "register-resident, twiddles in LDS; stage pairs 2..11)",
+                             "counter_issue_ms": ntt_issue_ms,
+                             "counter_issue_frac": round(ntt_issue_ms / ntt_ms, 4) if ntt_issue_ms and ntt_ms else None,
                              "pass_ms": round(ntt_pass_ms, 4) if ntt_pass_ms else None},
             "config4_msm_sharded": cfg4,
             "cpu_baseline": cpu,
@@ -667,24 +692,22 @@ def mix_leg(args, amd, torch, dev, rank, timed):
     g2p_same = bool(torch.equal(pres, res_iso))
     del table, pres
     acc_ms = g2_stage_ms(amd, torch, dev, g2, s_a)
-    i64 = pmc_counter("k_accumulate<G2>", "SQ_INSTS_VALU_INT64")
     contributions = 4 * n * ((64 + 16 - 1) // 16)  # psi split: 4n digit streams x 4 windows (c = 16)
-    mads = i64 * 64 if i64 else contributions * MADS_PER_G2_MADD
-    mad_t = mads / (acc_ms * 1e-3) / 1e12 if acc_ms else None
-    issue = valu_issue_bound_ms("k_accumulate<G2>")
+    ceil = valu_ceiling() or {}
+    cyc = (ceil.get("isa_2") or {}).get("simd_cycles_per_wave_instr")
+    issue = valu_issue_bound_ms("k_accumulate<G2>", cyc, (ceil.get("acc_ceiling") or {}).get("mhz_med"))
     return {"g2_msm_points": n, "ntt_batch": B, "ntt_size": nn, "g2_msm_ms": round(g2_ms, 3),
             "g2_msm_per_sec": round(1e3 / g2_ms, 3),
             "g2_prepared_bases_ms": round(g2p_ms, 3), "g2_prepared_equal_to_plain": g2p_same,
             "g2_roofline_hbm_frac": round(G2_BYTES_PER_POINT * n / (g2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
             "g2_accumulate_ms": round(acc_ms, 4) if acc_ms else None,
             "g2_roofline_valu": {"kernel": "k_accumulate<G2> (pair-sliced Fq2 lanes)", "bound": "valu",
-                                 "achieved": round(mad_t, 3) if mad_t else None, "peak": MAD_RATE_T,
-                                 "unit": "T v_mad_u64_u32/s",
-                                 "frac": round(mad_t / MAD_RATE_T, 4) if mad_t else None,
-                                 "mads_per_launch": round(mads),
-                                 "mads_source": "counter (SQ_INSTS_VALU_INT64 x 64)" if i64 else "algorithmic",
-                                 "counter_issue_bound_ms": round(issue, 4) if issue else None,
-                                 "counter_issue_frac": round(issue / acc_ms, 4) if issue and acc_ms else None},
+                                 "achieved": round(contributions / (acc_ms * 1e-3) / 1e9, 3) if acc_ms else None,
+                                 "unit": "G mixed additions/s",
+                                 "counter_issue_ms": round(issue, 4) if issue else None,
+                                 "counter_issue_frac": round(issue / acc_ms, 4) if issue and acc_ms else None,
+                                 "note": "counter_issue_ms = committed SQ_INSTS_VALU x the measured cycles per "
+                                         "wave-instruction (tools/valu_ceiling.hip) / 1024 SIMDs / measured clock"},
             "batched_ntt_ms": round(ntt_ms, 3), "overlapped_ms": round(both_ms, 3),
             "sum_isolated_ms": round(g2_ms + ntt_ms, 3), "streams": 2,
             "overlap_note": "both legs are VALU-bound (Montgomery products on v_mad_u64_u32), so two streams "
