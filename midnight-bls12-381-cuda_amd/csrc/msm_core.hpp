@@ -35,6 +35,7 @@
 
 #include "mbls_common.hpp"
 #include "mbls_curve.hpp"
+#include "mbls_fq28.hpp"
 #include "mbls_rowfield.hpp"
 #include "mbls_wavepoint.hpp"
 
@@ -283,6 +284,105 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
         }
     }
     store_jac<L>(partials, seg, acc);
+}
+
+// ------------------------------------------------------------------------------------
+// 4'. G1 accumulation in unsaturated radix 2^28 (mbls_fq28.hpp; round 5).  Same schedule as
+//     k_accumulate's LDS-DMA path -- chunks, bucket boundaries, the free first point and the
+//     mmadd second point, the next point staged in LDS -- with the lane arithmetic on 14 x 28-bit
+//     limbs: a column of a product is one v_mad_u64_u32 chain with no carry tracking (the 32-bit
+//     FIPS product pays a v_addc per mad, and on gfx950 every VALU instruction costs the same
+//     ~4 cycles: tools/valu_ceiling.hip).  Points are unpacked 8 bits low (x R 2^8 = x R',
+//     free), partials are written back in the library's canonical Montgomery words, so every
+//     other kernel is unchanged.  Same field values as jac_madd / jac_mmadd / jac_dbl, hence the
+//     same Jacobian partials, bit for bit (tools/fq28_bench.hip; the GPU parity suite).
+// ------------------------------------------------------------------------------------
+#ifndef MBLS_ACC_R28
+#define MBLS_ACC_R28 1
+#endif
+MBLS_DEV void store_jac28(uint8_t* __restrict__ partials, uint32_t seg, const r28::J28& acc) {
+    Jacobian<Fq> out;
+    if (acc.is_inf()) {
+        out = Jacobian<Fq>::inf();
+    } else {
+        r28::to_words(acc.x, out.x.v);
+        r28::to_words(acc.y, out.y.v);
+        r28::to_words(acc.z, out.z.v);
+    }
+    store_jac<Fq>(partials, seg, out);
+}
+
+#ifndef MBLS_ACC_R28_MINW
+#define MBLS_ACC_R28_MINW 3  // waves per SIMD the register budget is sized for (variant builds: 2)
+#endif
+template <class F>  // F = Fq only (a template so only msm_g1.hip instantiates it)
+__global__ __launch_bounds__(256, MBLS_ACC_R28_MINW) void k_accumulate_r28(const uint32_t* __restrict__ sorted,
+                                                           const uint32_t* __restrict__ offsets,
+                                                           const uint32_t* __restrict__ chunk_off,
+                                                           const uint32_t* __restrict__ first, uint32_t b0, uint32_t b1,
+                                                           const uint8_t* __restrict__ bases,
+                                                           const uint8_t* __restrict__ phi, uint32_t nsplit,
+                                                           uint32_t chunk, uint8_t* __restrict__ partials) {
+    const uint32_t gb = offsets[b0], ge = offsets[b1];
+    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) + gb / chunk;  // chunk index
+    uint32_t beg = t * chunk;
+    const uint32_t end = min(beg + chunk, ge);
+    beg = max(beg, gb);
+    if (beg >= end) return;
+    uint32_t b = first[t];
+    while (offsets[b + 1] <= beg) ++b;
+    uint32_t seg = chunk_off[b] + (t - offsets[b] / chunk);
+    uint32_t bend = offsets[b + 1];
+    r28::J28 acc = r28::J28::inf();
+    __shared__ uint4 stage[2][256 / 64][6][64];
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    auto issue = [&](uint32_t vv, uint32_t slot) {
+        uint32_t idx = vv >> 1;
+        const uint8_t* src = idx >= nsplit ? phi : bases;
+        idx = idx >= nsplit ? idx - nsplit : idx;
+        const uint8_t* g = src + (size_t)idx * 96;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(g + 16 * k),
+                                             (__attribute__((address_space(3))) void*)&stage[slot][wv][k][0], 16, 0, 0);
+    };
+    uint32_t v = sorted[beg];
+    issue(v, 0);
+    uint32_t vn = beg + 1 < end ? sorted[beg + 1] : v;
+    for (uint32_t e = beg; e < end; ++e) {
+        const uint32_t slot = (e - beg) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this point's pieces have landed
+        uint32_t xw[12], yw[12], any = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint4 xa = stage[slot][wv][k][ln], ya = stage[slot][wv][3 + k][ln];
+            xw[4 * k] = xa.x, xw[4 * k + 1] = xa.y, xw[4 * k + 2] = xa.z, xw[4 * k + 3] = xa.w;
+            yw[4 * k] = ya.x, yw[4 * k + 1] = ya.y, yw[4 * k + 2] = ya.z, yw[4 * k + 3] = ya.w;
+            any |= xa.x | xa.y | xa.z | xa.w | ya.x | ya.y | ya.z | ya.w;
+        }
+        if (e + 1 < end) issue(vn, slot ^ 1u);  // the other slot was read one addition ago
+        const uint32_t vnn = e + 2 < end ? sorted[e + 2] : vn;
+        if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
+            store_jac28(partials, seg, acc);
+            acc = r28::J28::inf();
+            do {
+                ++b;
+            } while (offsets[b + 1] == e);
+            seg = chunk_off[b];
+            bend = offsets[b + 1];
+        }
+        if (any) {  // the affine identity (0, 0) adds nothing
+            const r28::F28 qx = r28::unpack_shift8(xw);
+            r28::F28 qy = r28::unpack_shift8(yw);
+            if (v & 1) qy = r28::neg<r28::B512>(qy);  // -P: < 512 p, limbs < 2^30.4 (mbls_fq28.hpp)
+            bool done = false;
+            if (MBLS_ACC_MMADD && e == beg + 1 && !acc.is_inf()) done = r28::mmadd(acc, qx, qy);
+            if (!done) r28::madd(acc, qx, qy);
+        }
+        v = vn;
+        vn = vnn;
+    }
+    store_jac28(partials, seg, acc);
 }
 
 // ------------------------------------------------------------------------------------
@@ -907,6 +1007,7 @@ using AccKernel = void (*)(const uint32_t*, const uint32_t*, const uint32_t*, co
                            const uint8_t*, const uint8_t*, uint32_t, uint32_t, uint8_t*);
 template <class F>
 inline AccKernel accumulate_kernel() {
+    if (std::is_same<F, Fq>::value && MBLS_ACC_R28 && MBLS_ACC_LDS) return k_accumulate_r28<F>;
     if (std::is_same<F, Fq>::value && MBLS_ACC_W3) return k_accumulate<F, 3>;
     return k_accumulate<F, 1>;
 }
