@@ -319,22 +319,35 @@ MBLS_DEV J28 dbl(const J28& p) {
     return r;
 }
 
+// Register parking for the mixed addition: acc.x is needed again at V and acc.y at Y3, across
+// the products in between.  ParkReg keeps them in registers; a kernel at its register bound can
+// park them in memory it owns instead of letting the compiler spill to scratch (Park::put / get
+// of slot 0 = x, 1 = y; a park that holds only some slots keeps the others in registers).
+struct ParkReg {
+    F28 v[2];
+    MBLS_DEV void put(int s, const F28& a) { v[s] = a; }
+    MBLS_DEV F28 get(int s) const { return v[s]; }
+};
+
 // acc + q, q = (x2, y2) affine from unpack_shift8 (< 256 p, normalised, not the identity; y2
 // may instead be neg<B512> of one: < 512 p, limbs < 2^30.4 -- it only meets products and folds):
 // madd-2007-bl with the lazy Y3, Z3 = 2 Z1 H (the same field values as mbls_curve.hpp's
 // jac_madd, hence the same Jacobian representative)
-MBLS_DEV void madd(J28& acc, const F28& x2_, const F28& y2_) {
+template <class Park>
+MBLS_DEV void madd(J28& acc, const F28& x2_, const F28& y2_, Park& pk) {
     if (acc.is_inf()) {
         acc = {fold(x2_), fold(y2_), F28::one()};
         return;
     }
     const F28 Z1Z1 = sqr(acc.z);
-    const F28 U2 = mul(x2_, Z1Z1);
-    const F28 S2 = mul(mul(y2_, acc.z), Z1Z1);
-    const F28 H = sub<B16>(U2, acc.x);
-    const F28 R = sub<B16>(S2, acc.y);
+    const F28 H = sub<B16>(mul(x2_, Z1Z1), acc.x);
+    pk.put(0, acc.x);
+    const F28 R = sub<B16>(mul(mul(y2_, acc.z), Z1Z1), acc.y);
+    pk.put(1, acc.y);
     const F28 HH = sqr(H);
     if (is_zero_lt2p(HH)) {  // H == 0 mod p: equal or opposite points
+        acc.x = pk.get(0);
+        acc.y = pk.get(1);
         acc = is_zero_mod(R) ? dbl(acc) : J28::inf();
         return;
     }
@@ -342,10 +355,14 @@ MBLS_DEV void madd(J28& acc, const F28& x2_, const F28& y2_) {
     const F28 I = x4(HH);
     const F28 J = mul(H, I);
     acc.z = mul(x2(acc.z), H);
-    const F28 V = mul(acc.x, I);
+    const F28 V = mul(pk.get(0), I);
     const F28 R2 = carry(x2(R));
     acc.x = fold(sub<B32>(sub<B16>(sqr(R2), J), x2(V)));
-    acc.y = mul2(R2, sub<B16>(V, acc.x), neg<B32>(x2(acc.y)), J);
+    acc.y = mul2(R2, sub<B16>(V, acc.x), neg<B32>(x2(pk.get(1))), J);
+}
+MBLS_DEV void madd(J28& acc, const F28& x2_, const F28& y2_) {
+    ParkReg pk;
+    madd(acc, x2_, y2_, pk);
 }
 
 // acc fresh from the chunk's first point (z = R'-one, x, y folded): mmadd-2007-bl, Z3 = 2H.

@@ -312,6 +312,9 @@ MBLS_DEV void store_jac28(uint8_t* __restrict__ partials, uint32_t seg, const r2
     store_jac<Fq>(partials, seg, out);
 }
 
+#ifndef MBLS_ACC_R28_PARK
+#define MBLS_ACC_R28_PARK 1
+#endif
 #ifndef MBLS_ACC_R28_MINW
 #define MBLS_ACC_R28_MINW 3  // waves per SIMD the register budget is sized for (variant builds: 2)
 #endif
@@ -335,6 +338,41 @@ __global__ __launch_bounds__(256, MBLS_ACC_R28_MINW) void k_accumulate_r28(const
     uint32_t bend = offsets[b + 1];
     r28::J28 acc = r28::J28::inf();
     __shared__ uint4 stage[2][256 / 64][6][64];
+#if MBLS_ACC_R28_PARK
+    // acc.y parked in the lane's half of the stage that the current point was just read from
+    // (free until the next step's DMA), across the mixed addition's middle: 14 VGPRs fewer at
+    // the register bound, where the compiler otherwise spilled ~30 VGPRs to scratch
+    struct ParkStage {
+        uint4* q;  // this lane's 6 pieces of the free slot: stage[slot][wv][k][ln], stride 64
+        r28::F28 x;
+        MBLS_DEV void put(int s, const r28::F28& a) {
+            if (s == 0) {
+                x = a;
+                return;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                q[64 * k] = make_uint4(a.l[4 * k], a.l[4 * k + 1], k < 3 ? a.l[4 * k + 2] : 0u, k < 3 ? a.l[4 * k + 3] : 0u);
+            asm volatile("" ::: "memory");  // the register copy is dead: reload from LDS
+        }
+        MBLS_DEV r28::F28 get(int s) const {
+            if (s == 0) return x;
+            asm volatile("" ::: "memory");
+            r28::F28 r;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 u = q[64 * k];
+                r.l[4 * k] = u.x;
+                r.l[4 * k + 1] = u.y;
+                if (k < 3) {
+                    r.l[4 * k + 2] = u.z;
+                    r.l[4 * k + 3] = u.w;
+                }
+            }
+            return r;
+        }
+    };
+#endif
     const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     auto issue = [&](uint32_t vv, uint32_t slot) {
         uint32_t idx = vv >> 1;
@@ -377,7 +415,12 @@ __global__ __launch_bounds__(256, MBLS_ACC_R28_MINW) void k_accumulate_r28(const
             if (v & 1) qy = r28::neg<r28::B512>(qy);  // -P: < 512 p, limbs < 2^30.4 (mbls_fq28.hpp)
             bool done = false;
             if (MBLS_ACC_MMADD && e == beg + 1 && !acc.is_inf()) done = r28::mmadd(acc, qx, qy);
-            if (!done) r28::madd(acc, qx, qy);
+#if MBLS_ACC_R28_PARK
+            ParkStage pk{&stage[slot][wv][0][ln]};
+#else
+            r28::ParkReg pk;
+#endif
+            if (!done) r28::madd(acc, qx, qy, pk);
         }
         v = vn;
         vn = vnn;
