@@ -365,6 +365,34 @@ MBLS_DEV void madd(J28& acc, const F28& x2_, const F28& y2_) {
     madd(acc, x2_, y2_, pk);
 }
 
+// acc + q for a Jacobian q = (x2, y2, z2) from unpack_shift8 (each < 256 p, normalised; z2 != 0):
+// add-2007-bl with the lazy Y3 and Z3 = 2 Z1 Z2 H (the field values of mbls_curve.hpp's jac_add,
+// hence the same representative).  Bounds as in madd; Z2Z2 of an unpacked z2 is < 27 p.
+MBLS_DEV void jadd(J28& acc, const F28& x2_, const F28& y2_, const F28& z2_) {
+    if (acc.is_inf()) {
+        acc = {fold(x2_), fold(y2_), fold(z2_)};
+        return;
+    }
+    const F28 Z1Z1 = sqr(acc.z);
+    const F28 Z2Z2 = sqr(z2_);
+    const F28 U1 = mul(acc.x, Z2Z2);
+    const F28 S1 = mul(mul(acc.y, z2_), Z2Z2);
+    const F28 H = sub<B16>(mul(x2_, Z1Z1), U1);
+    const F28 R = sub<B16>(mul(mul(y2_, acc.z), Z1Z1), S1);
+    const F28 HH = sqr(H);
+    if (is_zero_lt2p(HH)) {  // H == 0 mod p: equal or opposite points
+        acc = is_zero_mod(R) ? dbl(acc) : J28::inf();
+        return;
+    }
+    const F28 I = x4(HH);
+    const F28 J = mul(H, I);
+    acc.z = mul(mul(x2(acc.z), z2_), H);
+    const F28 V = mul(U1, I);
+    const F28 R2 = carry(x2(R));
+    acc.x = fold(sub<B32>(sub<B16>(sqr(R2), J), x2(V)));
+    acc.y = mul2(R2, sub<B16>(V, acc.x), neg<B32>(x2(S1)), J);
+}
+
 // acc fresh from the chunk's first point (z = R'-one, x, y folded): mmadd-2007-bl, Z3 = 2H.
 // Returns false (acc untouched) when x1 == x2 mod p, left to madd's branches.
 MBLS_DEV bool mmadd(J28& acc, const F28& x2_, const F28& y2_) {

@@ -300,6 +300,9 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
 #ifndef MBLS_ACC_R28
 #define MBLS_ACC_R28 1
 #endif
+#ifndef MBLS_BS_R28
+#define MBLS_BS_R28 1  // light bucket sums (k_bucket_small, G1) in radix 2^28 too
+#endif
 MBLS_DEV void store_jac28(uint8_t* __restrict__ partials, uint32_t seg, const r28::J28& acc) {
     Jacobian<Fq> out;
     if (acc.is_inf()) {
@@ -611,6 +614,26 @@ __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32
     if (t >= stop) return;
     const uint32_t b = perm[t];
     const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
+    if constexpr (std::is_same<L, Fq>::value && MBLS_BS_R28) {
+        // radix 2^28 (mbls_fq28.hpp jadd; same values as jac_add, round 5)
+        r28::J28 acc = r28::J28::inf();
+        for (uint32_t k = k0; k < k1; ++k) {
+            const uint4* q = reinterpret_cast<const uint4*>(partials + (size_t)k * 144);
+            uint32_t w[3][12], zany = 0;
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const uint4 u = q[3 * c + j];
+                    w[c][4 * j] = u.x, w[c][4 * j + 1] = u.y, w[c][4 * j + 2] = u.z, w[c][4 * j + 3] = u.w;
+                }
+#pragma unroll
+            for (int j = 0; j < 12; ++j) zany |= w[2][j];
+            if (zany) r28::jadd(acc, r28::unpack_shift8(w[0]), r28::unpack_shift8(w[1]), r28::unpack_shift8(w[2]));
+        }
+        store_jac28(buckets, b, acc);
+        return;
+    }
     Jacobian<L> acc = Jacobian<L>::inf();
     if (k1 > k0) acc = load_jac<L>(partials, k0);
     for (uint32_t k = k0 + 1; k < k1; ++k) acc = jac_add(acc, load_jac<L>(partials, k));

@@ -48,6 +48,11 @@ namespace mbls {
 #ifndef MBLS_NTT_XCD
 #define MBLS_NTT_XCD 0  // 1: tiles of adjacent columns on the same XCD (shared L2 lines)
 #endif
+// diagnostic variant builds only (results WRONG, never shipped): 1 = no twiddle loads (a
+// register value instead), 2 = no barrier between stage pairs -- to price those costs
+#ifndef MBLS_NTT_EXP
+#define MBLS_NTT_EXP 0
+#endif
 static constexpr int NTT_TILE_LOG = MBLS_NTT_TILE_LOG;
 static constexpr int NTT_TILE = 1 << NTT_TILE_LOG;  // elements per workgroup tile
 static constexpr int NTT_THREADS = MBLS_NTT_THREADS;
@@ -218,7 +223,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ 
             // stage l: (x0, x1), (x2, x3) share twiddle w_(2^s)^j; trivial for j = 0 in the first
             // pass (always at s = 1: h = 1)
             if (!(FIRST && l == 1)) {
-                const Fr w1 = load<FrCfg>(tw1 + 32 * (((size_t)j << s0) + lo));
+                const Fr w1 = MBLS_NTT_EXP == 1 ? x2 : load<FrCfg>(tw1 + 32 * (((size_t)j << s0) + lo));
                 x1 = fips::mul<FrCfg, false>(x1, w1);
                 x3 = fips::mul<FrCfg, false>(x3, w1);
             }
@@ -226,17 +231,17 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ 
             // stage l + 1: (y0, y2) with w_(2^(s+1))^j (trivial in the first pair of the first
             // pass: j = 0), (y1, y3) with w_(2^(s+1))^(j + h)
             if (!(FIRST && l == 1)) {
-                const Fr w2 = load<FrCfg>(tw2 + 32 * (((size_t)j << s0) + lo));
+                const Fr w2 = MBLS_NTT_EXP == 1 ? x0 : load<FrCfg>(tw2 + 32 * (((size_t)j << s0) + lo));
                 y2 = fips::mul<FrCfg, false>(y2, w2);
             }
-            const Fr w3 = load<FrCfg>(tw2 + 32 * (((size_t)(j + h) << s0) + lo));
+            const Fr w3 = MBLS_NTT_EXP == 1 ? x0 : load<FrCfg>(tw2 + 32 * (((size_t)(j + h) << s0) + lo));
             y3 = fips::mul<FrCfg, false>(y3, w3);
             store<FrCfg>(p0, add_2r(y0, y2));
             store<FrCfg>(p0 + 2 * stride, sub_2r(y0, y2));
             store<FrCfg>(p0 + stride, add_2r(y1, y3));
             store<FrCfg>(p0 + 3 * stride, sub_2r(y1, y3));
         }
-        __syncthreads();
+        if (MBLS_NTT_EXP != 2) __syncthreads();
     }
     if (l == L) {  // odd stage count: one radix-2 stage
         const int half = 1 << (l - 1);
