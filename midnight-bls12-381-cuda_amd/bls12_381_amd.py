@@ -77,7 +77,7 @@ EXPORTED = [
     "mbls_release_stream", "mbls_release_scratch", "mbls_scratch_stats",
     "mbls_g1_msm_multi_device", "mbls_g2_msm_multi_device", "bls12_381_vector_sum",
     "bls12_381_g1_affine_to_projective", "bls12_381_g1_projective_to_affine", "bls12_381_g2_projective_to_affine",
-    "mbls_msm_plan",
+    "mbls_msm_plan", "mbls_msm_accumulate_event",
 ]
 
 _LIB = None
@@ -121,6 +121,7 @@ def lib():
         "bls12_381_g1_affine_to_projective": [P, i32, P, P], "bls12_381_g1_projective_to_affine": [P, i32, P, P],
         "bls12_381_g2_projective_to_affine": [P, i32, P, P],
         "mbls_msm_plan": [i32, i32, P, P],
+        "mbls_msm_accumulate_event": [P, P],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -395,6 +396,41 @@ def msm_multi_device(group, scalars, bases_per_dev, devs, n, *, scalars_mont=Tru
     fn = lib().mbls_g1_msm_multi_device if group == "g1" else lib().mbls_g2_msm_multi_device
     check(fn(_p(scalars), ptrs, dv, k, n, ctypes.byref(cfg), _p(out)), f"{group} msm_multi_device")
     return out
+
+
+def msm_accumulate_event(stream, event):
+    """mbls_msm_accumulate_event: the next single MSM on `stream` records the raw hipEvent_t
+    `event` (an int handle, or None to clear) when its accumulation is enqueued (its tail starts)"""
+    check(lib().mbls_msm_accumulate_event(_stream_handle(stream), ctypes.c_void_p(event) if event else None),
+          "mbls_msm_accumulate_event")
+
+
+class HipEvent:
+    """a raw hipEvent_t (timing disabled) that another stream can wait on (hipStreamWaitEvent)"""
+
+    def __init__(self):
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        self.hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self.hip.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+        self.ev = ctypes.c_void_p()
+        if self.hip.hipEventCreateWithFlags(ctypes.byref(self.ev), 2) != 0:  # hipEventDisableTiming
+            raise RuntimeError("hipEventCreateWithFlags failed")
+
+    @property
+    def handle(self):
+        return self.ev.value
+
+    def wait(self, stream):
+        """make `stream` (torch stream) wait for the event"""
+        if self.hip.hipStreamWaitEvent(_stream_handle(stream), self.ev, 0) != 0:
+            raise RuntimeError("hipStreamWaitEvent failed")
+
+    def __del__(self):
+        try:
+            self.hip.hipEventDestroy(self.ev)
+        except Exception:
+            pass
 
 
 def scratch_stats():

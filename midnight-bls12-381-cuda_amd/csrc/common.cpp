@@ -299,6 +299,23 @@ static void profile_drain() {
 
 }  // namespace mbls
 
+// mbls_msm_accumulate_event: one pending event per stream, taken by the next MSM on it
+namespace mbls {
+static std::mutex g_acc_ev_mu;
+static std::map<hipStream_t, hipEvent_t>* g_acc_ev = new std::map<hipStream_t, hipEvent_t>();
+static std::atomic<int> g_acc_ev_n{0};
+hipEvent_t take_accumulate_event(hipStream_t st) {
+    if (g_acc_ev_n.load(std::memory_order_relaxed) == 0) return nullptr;  // the hot path: nothing pending
+    std::lock_guard<std::mutex> g(g_acc_ev_mu);
+    auto it = g_acc_ev->find(st);
+    if (it == g_acc_ev->end()) return nullptr;
+    hipEvent_t e = it->second;
+    g_acc_ev->erase(it);
+    g_acc_ev_n.fetch_sub(1, std::memory_order_relaxed);
+    return e;
+}
+}  // namespace mbls
+
 extern "C" {
 
 void mbls_profile_enable(int on) {
@@ -329,6 +346,22 @@ int mbls_profile_read(const char** names, double* total_ms, long* counts, int ma
 }
 
 /* scratch pool (include/bls12_381_mi355x.h) */
+
+eIcicleError mbls_msm_accumulate_event(void* stream, void* event) {
+    std::lock_guard<std::mutex> g(mbls::g_acc_ev_mu);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    auto it = mbls::g_acc_ev->find(st);
+    if (it != mbls::g_acc_ev->end()) {
+        mbls::g_acc_ev->erase(it);
+        mbls::g_acc_ev_n.fetch_sub(1, std::memory_order_relaxed);
+    }
+    if (event) {
+        (*mbls::g_acc_ev)[st] = static_cast<hipEvent_t>(event);
+        mbls::g_acc_ev_n.fetch_add(1, std::memory_order_relaxed);
+    }
+    return MBLS_SUCCESS;
+}
+
 eIcicleError mbls_release_stream(void* stream) {
     mbls::Pool& P = mbls::pool();
     std::lock_guard<std::mutex> g(P.mu);

@@ -116,6 +116,8 @@ const void* pinned_host_device_pointer(const void* p);
 // bytes from `p` to the end of the device allocation holding it (hipMemGetAddressRange), or
 // SIZE_MAX when the runtime cannot tell (host memory, foreign allocators)
 size_t device_bytes_from(const void* p);
+// the event mbls_msm_accumulate_event left pending for `st` (taken: nullptr afterwards), or nullptr
+hipEvent_t take_accumulate_event(hipStream_t st);
 
 // Stage profiler: when enabled (mbls_profile_enable / MBLS_PROFILE=1) a ProfScope records a
 // hipEvent pair on the stream around the enclosed launches; mbls_profile_read() sums the

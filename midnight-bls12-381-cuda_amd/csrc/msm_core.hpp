@@ -1302,6 +1302,9 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         hipLaunchKernelGGL(accumulate_kernel<F>(), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
                            chunk_off, first, 0u, TB, acc_b, acc_phi, nsplit, P.chunk, partials);
     }
+    if (!pipe) {  // mbls_msm_accumulate_event: the tail starts here (single MSMs only)
+        if (hipEvent_t ev = take_accumulate_event(st)) MBLS_TRY(hipEventRecord(ev, st));
+    }
     {
         ProfScope ps("msm.bucket_sum", st);
         // light buckets one thread each, heavy buckets by slice workgroups in the same launch

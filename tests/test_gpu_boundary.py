@@ -243,3 +243,39 @@ def test_precompute_factor_on_plain_device_bases(amd, gh, hip, group):
             assert np.array_equal(r, ref), F
     finally:
         raw.free()
+
+
+def test_msm_accumulate_event_orders_a_second_stream(amd, gh):
+    """mbls_msm_accumulate_event (config #5's overlap): the next MSM on the stream records the
+    event once its accumulation is enqueued; an NTT on another stream waits on it.  Both results
+    equal their isolated runs (MSM against the oracle), the pending event is taken by exactly one
+    MSM, and clearing it (NULL) leaves the next MSM without one."""
+    import torch
+    n, nn = (1 << 12) + 3, 1 << 14
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0B41, montgomery=True)
+    b = torch.zeros((n, 24), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g2", b, 0x5EED0B42)
+    x = torch.zeros((nn, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(x, 0x5EED0B43, montgomery=True)
+    amd.ntt_init_domain()
+    torch.cuda.synchronize()
+    ref_ntt = amd.to_numpy_u64(amd.ntt(x, out=torch.zeros_like(x)))
+    ref = H.g2_from_affine_mont(H.oracle_msm("g2", _std_scalars(0x5EED0B41, n), amd.to_numpy_u64(b),
+                                             threads=ORACLE_THREADS))
+    s_a, s_b = torch.cuda.Stream(priority=-1), torch.cuda.Stream()
+    ev = amd.HipEvent()
+    for rep in range(3):
+        out = torch.zeros((1, 36), dtype=torch.int64, device="cuda")
+        y = torch.zeros_like(x)
+        amd.msm_accumulate_event(s_a, ev.handle)
+        amd.msm("g2", s, b, scalars_mont=True, out=out, stream=s_a, is_async=True, n=n)
+        ev.wait(s_b)
+        amd.ntt(x, out=y, stream=s_b, is_async=True)
+        torch.cuda.synchronize()
+        assert gh.decode_icicle("g2", amd.to_numpy_u64(out)[0]) == ref, rep
+        assert np.array_equal(amd.to_numpy_u64(y), ref_ntt), rep
+    amd.msm_accumulate_event(s_a, ev.handle)
+    amd.msm_accumulate_event(s_a, None)  # cleared: the next MSM records nothing
+    r = amd.msm("g2", s, b, scalars_mont=True, stream=s_a, n=n)
+    assert gh.decode_icicle("g2", r[0]) == ref

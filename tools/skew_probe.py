@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--group", default="g1")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cases", default="")
+    ap.add_argument("--stages", action="store_true", help="also print the stage profiler's ms per stage")
     a = ap.parse_args()
     import torch
     import bls12_381_amd as amd
@@ -67,6 +68,15 @@ def main():
         torch.cuda.synchronize()
         row[name] = round((time.perf_counter() - t0) / a.reps * 1e3, 3)
         print(json.dumps(row), flush=True)
+        if a.stages:
+            amd.profile(True)
+            for _ in range(3):
+                call()
+            torch.cuda.synchronize()
+            prof = amd.profile_read()
+            amd.profile(False)
+            print(json.dumps({"case": name, "stage_ms": {k: round(v[0] / v[1], 4) for k, v in sorted(prof.items()) if v[1]}}),
+                  flush=True)
 
 
 if __name__ == "__main__":
