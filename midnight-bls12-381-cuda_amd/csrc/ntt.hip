@@ -131,8 +131,8 @@ __global__ void k_twiddles(uint8_t* table, Fr w, int L, uint32_t count) {
 // Montgomery product needs no final subtraction (fips::mul<C, false>); a + t and a - t are
 // brought back into [0, 2r) with one conditional 2r correction each (same cost as the
 // canonical add / sub).  The last pass stores canonical values.
-__constant__ uint32_t NTT_TWO_R[8] = {0x00000002u, 0xfffffffeu, 0xfffcb7fdu, 0xa77b4805u,
-                                      0x1343b00au, 0x6673b010u, 0x533afa90u, 0xe7db4ea6u};
+static constexpr uint32_t NTT_TWO_R[8] = {0x00000002u, 0xfffffffeu, 0xfffcb7fdu, 0xa77b4805u,
+                                          0x1343b00au, 0x6673b010u, 0x533afa90u, 0xe7db4ea6u};  // literals
 MBLS_DEV Fr add_2r(const Fr& a, const Fr& b) {
     Fr s, d;
     unsigned c = 0, br = 0;
@@ -156,140 +156,143 @@ MBLS_DEV Fr sub_2r(const Fr& a, const Fr& b) {
     return d;
 }
 
+// an Fr element as two 16-byte words (LDS tile, global data, twiddle tables): element e at
+// [2e], [2e + 1] -- 32-bit element indices (transforms <= 2^30, ntt_call) and b128 accesses
+MBLS_DEV Fr ld2(const uint4* p, uint32_t e) {
+    const uint4 a = p[2 * e], b = p[2 * e + 1];
+    return Fr{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+}
+MBLS_DEV void st2(uint4* p, uint32_t e, const Fr& v) {
+    p[2 * e] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+    p[2 * e + 1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+}
+
 // One pass of up to NTT_TILE_LOG DIT stages.
 //   FIRST: stages 1..L with the bit-reversal gather from `in`; else stages s0+1..s0+L in place.
 //   LAST:  store canonical values; SCALE (inverse, implies LAST): multiply them by n^-1.
+// Index arithmetic is 32-bit (element indices inside a polynomial and the twiddle tables stay
+// below 2^31 for transforms <= 2^30), the tile is a uint4 LDS array (every access one b128),
+// and the 2r constants are literals: round 5 trimmed ~10% non-arithmetic instructions this way
+// (the pass is VALU-issue bound, profiles/r05/ntt_diag.txt).
 template <bool FIRST, bool LAST, bool SCALE>
-__global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ out, const uint8_t* __restrict__ in,
-                                                          const uint8_t* __restrict__ tw, int log_n, int s0, int L,
+__global__ __launch_bounds__(NTT_THREADS) void k_ntt_pass(uint8_t* __restrict__ out_, const uint8_t* __restrict__ in_,
+                                                          const uint8_t* __restrict__ tw_, int log_n, int s0, int L,
                                                           int logC, Fr scale) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[NTT_TILE * 32];
-    const int C = 1 << logC;
-    const int rows = 1 << L;
-    const int T = rows * C;  // active tile elements (== NTT_TILE except for tiny transforms)
+    __shared__ uint4 lds[NTT_TILE * 2];
+    const uint32_t C = 1u << logC;
+    const uint32_t rows = 1u << L;
+    const uint32_t T = rows * C;  // active tile elements (== NTT_TILE except for tiny transforms)
     const size_t n = (size_t)1 << log_n;
-    const int tiles_per_poly = (int)(n >> (L + logC));
-    int bid = (int)blockIdx.x;
-    if (MBLS_NTT_XCD && (gridDim.x & 7) == 0) bid = (bid & 7) * (int)(gridDim.x >> 3) + (bid >> 3);
-    const int poly = bid / tiles_per_poly;
-    const int tile = bid % tiles_per_poly;
-    const size_t pbase = (size_t)poly * n;
+    const uint32_t tiles_per_poly = (uint32_t)(n >> (L + logC));
+    uint32_t bid = blockIdx.x;
+    if (MBLS_NTT_XCD && (gridDim.x & 7) == 0) bid = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);
+    const uint32_t poly = bid / tiles_per_poly;
+    const uint32_t tile = bid % tiles_per_poly;
+    uint4* out = reinterpret_cast<uint4*>(out_) + 2 * (size_t)poly * n;
+    const uint4* in = reinterpret_cast<const uint4*>(FIRST ? in_ : out_) + 2 * (size_t)poly * n;
+    const uint4* tw = reinterpret_cast<const uint4*>(tw_);
+    // FIRST: element (row tr, column c0 + c) at (tr << colbits) + c0 + c; else element (t, c) at
+    // hi_base + (t << s0) + lo0 + c
+    const uint32_t colbits = (uint32_t)(log_n - L);
+    const uint32_t lo_tiles = FIRST ? 1u : (1u << s0) >> logC;
+    const uint32_t lo0 = FIRST ? tile * C : (tile % lo_tiles) * C;
+    const uint32_t hi_base = FIRST ? 0u : (tile / lo_tiles) << (s0 + L);
 
-    // ---- load tile into LDS as [row t][col c]
-    if (FIRST) {
-        // input viewed as 2^L rows x 2^(k-L) cols; tile = cols [c0, c0 + C)
-        const int colbits = log_n - L;
-        const size_t c0 = (size_t)tile * C;
-        for (int e = threadIdx.x; e < T; e += NTT_THREADS) {
-            int c = e & (C - 1), tr = e >> logC;  // source row tr
-            size_t src = pbase + ((size_t)tr << colbits) + c0 + c;
-            Fr v = load<FrCfg>(in + 32 * src);
-            int p = (int)bitrev((uint32_t)tr, L);  // DIT position inside the block
-            store<FrCfg>(lds + 32 * (p * C + c), v);
-        }
-    } else {
-        // rows t: stride 2^s0; cols lo in [lo0, lo0 + C) inside the low 2^s0 block
-        const int lo_tiles = (int)(((size_t)1 << s0) >> logC);
-        const size_t hi = tile / lo_tiles;
-        const size_t lo0 = (size_t)(tile % lo_tiles) * C;
-        for (int e = threadIdx.x; e < T; e += NTT_THREADS) {
-            int c = e & (C - 1), t = e >> logC;
-            size_t idx = pbase + (hi << (s0 + L)) + ((size_t)t << s0) + lo0 + c;
-            Fr v = load<FrCfg>(out + 32 * idx);
-            store<FrCfg>(lds + 32 * e, v);
+    // ---- load tile into LDS as [row t][col c] (not vectorised: the loop vectoriser split the
+    // b128 LDS stores of two elements into 16 ds_write_b32)
+#pragma clang loop vectorize(disable) interleave(disable)
+    for (uint32_t e = threadIdx.x; e < T; e += NTT_THREADS) {
+        const uint32_t c = e & (C - 1), t = e >> logC;
+        if (FIRST) {
+            st2(lds, bitrev(t, L) * C + c, ld2(in, (t << colbits) + lo0 + c));  // DIT position
+        } else {
+            st2(lds, e, ld2(in, hi_base + (t << s0) + lo0 + c));
         }
     }
     __syncthreads();
 
     // ---- L DIT stages: pairs of stages as radix-4 (2 x 2) butterflies in registers (one LDS
     // round trip and one barrier per pair), an odd last stage as radix-2
-    const size_t lo_base = FIRST ? 0 : (size_t)(tile % (int)(((size_t)1 << s0) >> logC)) * C;
+    const uint32_t lo_base = FIRST ? 0u : lo0;
     int l = 1;
     for (; l + 1 <= L; l += 2) {
-        const int h = 1 << (l - 1);  // stage l pairs rows (t, t + h), stage l + 1 rows (t, t + 2h)
-        const int s = s0 + l;        // global stage of the first of the pair
-        const uint8_t* tw1 = tw + 32 * (((size_t)1 << (s - 1)) - 1);
-        const uint8_t* tw2 = tw + 32 * (((size_t)1 << s) - 1);
-        for (int u = threadIdx.x; u < T / 4; u += NTT_THREADS) {
-            const int c = u & (C - 1);
-            const int r = u >> logC;
-            const int j = r & (h - 1);
-            const int q = ((r >> (l - 1)) << (l + 1)) + j;
-            uint8_t* p0 = lds + 32 * (q * C + c);
-            const size_t stride = (size_t)32 * h * C;
-            Fr x0 = load<FrCfg>(p0), x1 = load<FrCfg>(p0 + stride), x2 = load<FrCfg>(p0 + 2 * stride),
-               x3 = load<FrCfg>(p0 + 3 * stride);
-            const size_t lo = FIRST ? 0 : lo_base + c;
-            // stage l: (x0, x1), (x2, x3) share twiddle w_(2^s)^j; trivial for j = 0 in the first
-            // pass (always at s = 1: h = 1)
-            if (!(FIRST && l == 1)) {
-                const Fr w1 = MBLS_NTT_EXP == 1 ? x2 : load<FrCfg>(tw1 + 32 * (((size_t)j << s0) + lo));
+        const uint32_t h = 1u << (l - 1);  // stage l pairs rows (t, t + h), stage l + 1 rows (t, t + 2h)
+        const int s = s0 + l;              // global stage of the first of the pair
+        const uint4* tw1 = tw + 2 * ((1u << (s - 1)) - 1);
+        const uint4* tw2 = tw + 2 * ((1u << s) - 1);
+        const uint32_t stride = h * C;
+        for (uint32_t u = threadIdx.x; u < T / 4; u += NTT_THREADS) {
+            const uint32_t c = u & (C - 1);
+            const uint32_t r = u >> logC;
+            const uint32_t j = r & (h - 1);
+            const uint32_t q = ((r >> (l - 1)) << (l + 1)) + j;
+            const uint32_t e0 = q * C + c;
+            const uint32_t lo = FIRST ? 0u : lo_base + c;
+            const bool triv = FIRST && l == 1;  // first pair of the first pass: j = 0, twiddles 1
+            // twiddles first: their loads do not depend on the tile
+            Fr w1, w2, w3;
+            if (!triv) {
+                w1 = ld2(tw1, (j << s0) + lo);
+                w2 = ld2(tw2, (j << s0) + lo);
+            }
+            w3 = ld2(tw2, ((j + h) << s0) + lo);
+            Fr x0 = ld2(lds, e0), x1 = ld2(lds, e0 + stride), x2 = ld2(lds, e0 + 2 * stride),
+               x3 = ld2(lds, e0 + 3 * stride);
+            if (MBLS_NTT_EXP == 1) w1 = w2 = w3 = x0;
+            // stage l: (x0, x1), (x2, x3) share twiddle w_(2^s)^j
+            if (!triv) {
                 x1 = fips::mul<FrCfg, false>(x1, w1);
                 x3 = fips::mul<FrCfg, false>(x3, w1);
             }
             Fr y0 = add_2r(x0, x1), y1 = sub_2r(x0, x1), y2 = add_2r(x2, x3), y3 = sub_2r(x2, x3);
-            // stage l + 1: (y0, y2) with w_(2^(s+1))^j (trivial in the first pair of the first
-            // pass: j = 0), (y1, y3) with w_(2^(s+1))^(j + h)
-            if (!(FIRST && l == 1)) {
-                const Fr w2 = MBLS_NTT_EXP == 1 ? x0 : load<FrCfg>(tw2 + 32 * (((size_t)j << s0) + lo));
-                y2 = fips::mul<FrCfg, false>(y2, w2);
-            }
-            const Fr w3 = MBLS_NTT_EXP == 1 ? x0 : load<FrCfg>(tw2 + 32 * (((size_t)(j + h) << s0) + lo));
+            // stage l + 1: (y0, y2) with w_(2^(s+1))^j, (y1, y3) with w_(2^(s+1))^(j + h)
+            if (!triv) y2 = fips::mul<FrCfg, false>(y2, w2);
             y3 = fips::mul<FrCfg, false>(y3, w3);
-            store<FrCfg>(p0, add_2r(y0, y2));
-            store<FrCfg>(p0 + 2 * stride, sub_2r(y0, y2));
-            store<FrCfg>(p0 + stride, add_2r(y1, y3));
-            store<FrCfg>(p0 + 3 * stride, sub_2r(y1, y3));
+            st2(lds, e0, add_2r(y0, y2));
+            st2(lds, e0 + 2 * stride, sub_2r(y0, y2));
+            st2(lds, e0 + stride, add_2r(y1, y3));
+            st2(lds, e0 + 3 * stride, sub_2r(y1, y3));
         }
         if (MBLS_NTT_EXP != 2) __syncthreads();
     }
     if (l == L) {  // odd stage count: one radix-2 stage
-        const int half = 1 << (l - 1);
+        const uint32_t half = 1u << (l - 1);
         const int s = s0 + l;  // global stage, m = 2^s
-        for (int u = threadIdx.x; u < T / 2; u += NTT_THREADS) {
-            int c = u & (C - 1);
-            int r = u >> logC;
-            int g = r >> (l - 1);
-            int j = r & (half - 1);
-            int t0 = (g << l) + j;
-            int t1 = t0 + half;
-            Fr a = load<FrCfg>(lds + 32 * (t0 * C + c));
-            Fr b = load<FrCfg>(lds + 32 * (t1 * C + c));
-            if (l > 1 || !FIRST) {
-                size_t jj = ((size_t)j << s0) + (FIRST ? 0 : lo_base + c);
-                Fr w = load<FrCfg>(tw + 32 * ((((size_t)1 << (s - 1)) - 1) + jj));
-                b = fips::mul<FrCfg, false>(b, w);
-            }
-            store<FrCfg>(lds + 32 * (t0 * C + c), add_2r(a, b));
-            store<FrCfg>(lds + 32 * (t1 * C + c), sub_2r(a, b));
+        const uint4* tws = tw + 2 * ((1u << (s - 1)) - 1);
+        for (uint32_t u = threadIdx.x; u < T / 2; u += NTT_THREADS) {
+            const uint32_t c = u & (C - 1);
+            const uint32_t r = u >> logC;
+            const uint32_t g = r >> (l - 1);
+            const uint32_t j = r & (half - 1);
+            const uint32_t t0 = (g << l) + j, t1 = t0 + half;
+            Fr w;
+            if (l > 1 || !FIRST) w = ld2(tws, (j << s0) + (FIRST ? 0u : lo_base + c));
+            const Fr a = ld2(lds, t0 * C + c);
+            Fr b = ld2(lds, t1 * C + c);
+            if (l > 1 || !FIRST) b = fips::mul<FrCfg, false>(b, w);
+            st2(lds, t0 * C + c, add_2r(a, b));
+            st2(lds, t1 * C + c, sub_2r(a, b));
         }
         __syncthreads();
     }
 
     // ---- store
-    if (FIRST) {
-        const int colbits = log_n - L;
-        const size_t c0 = (size_t)tile * C;
-        for (int e = threadIdx.x; e < T; e += NTT_THREADS) {
+    for (uint32_t e = threadIdx.x; e < T; e += NTT_THREADS) {
+        Fr v;
+        uint32_t dst;
+        if (FIRST) {
             // write block by block: consecutive threads -> consecutive positions of one block
-            int p = e & (rows - 1), c = e >> L;
-            size_t blk = bitrev((uint32_t)(c0 + c), colbits);
-            Fr v = load<FrCfg>(lds + 32 * (p * C + c));
-            if (SCALE) v = v * scale;  // v < 2r, scale < r: the reduced product is canonical
-            else if (LAST) reduce_once(v);
-            store<FrCfg>(out + 32 * (pbase + (blk << L) + p), v);
+            const uint32_t p = e & (rows - 1), c = e >> L;
+            v = ld2(lds, p * C + c);
+            dst = (bitrev(lo0 + c, colbits) << L) + p;
+        } else {
+            const uint32_t c = e & (C - 1), t = e >> logC;
+            v = ld2(lds, e);
+            dst = hi_base + (t << s0) + lo0 + c;
         }
-    } else {
-        const int lo_tiles = (int)(((size_t)1 << s0) >> logC);
-        const size_t hi = tile / lo_tiles;
-        const size_t lo0 = (size_t)(tile % lo_tiles) * C;
-        for (int e = threadIdx.x; e < T; e += NTT_THREADS) {
-            int c = e & (C - 1), t = e >> logC;
-            Fr v = load<FrCfg>(lds + 32 * e);
-            if (SCALE) v = v * scale;
-            else if (LAST) reduce_once(v);
-            store<FrCfg>(out + 32 * (pbase + (hi << (s0 + L)) + ((size_t)t << s0) + lo0 + c), v);
-        }
+        if (SCALE) v = v * scale;  // v < 2r, scale < r: the reduced product is canonical
+        else if (LAST) reduce_once(v);
+        st2(out, dst, v);
     }
 }
 
