@@ -1439,18 +1439,18 @@ MBLS_DEV void lds_count(uint32_t* cnt, uint32_t key) {
 #define MBLS_PS_U 16  // G1 2^20 all-1 scalars: 1.55 / 1.49 / 1.46 ms with 4 / 8 / 16; random unchanged
 #endif
 static constexpr uint32_t PS_U = MBLS_PS_U;
-template <bool PACK, class Fn>
+template <bool PACK, uint32_t TEAM = PS_TEAM, class Fn>
 MBLS_DEV void part_walk(const uint32_t* __restrict__ ent, size_t o, uint32_t k, uint32_t tl, int FB, Fn&& fn) {
-    for (uint32_t i = tl; i < k; i += PS_U * PS_TEAM) {
+    for (uint32_t i = tl; i < k; i += PS_U * TEAM) {
         uint32_t fine[PS_U], val[PS_U];
         // unconditional loads (a clamped index past the segment's end): straight-line code keeps
         // all PS_U loads in flight together
 #pragma unroll
         for (uint32_t u = 0; u < PS_U; ++u)
-            part_entry<PACK>(ent, o + min(i + u * PS_TEAM, k - 1), FB, fine[u], val[u]);
+            part_entry<PACK>(ent, o + min(i + u * TEAM, k - 1), FB, fine[u], val[u]);
 #pragma unroll
         for (uint32_t u = 0; u < PS_U; ++u)
-            if (i + u * PS_TEAM < k) fn(fine[u], val[u]);
+            if (i + u * TEAM < k) fn(fine[u], val[u]);
     }
 }
 
@@ -1464,16 +1464,182 @@ MBLS_DEV void part_walk(const uint32_t* __restrict__ ent, size_t o, uint32_t k, 
 static constexpr uint32_t PS_THREADS = MBLS_PS_THREADS;
 static_assert(PS_THREADS % 64 == 0 && PS_THREADS <= 1024 && PS_THREADS >= 256, "MBLS_PS_THREADS");
 
+// ---- heavy parts (skewed scalars, round 5) ----
+// A part holding far more entries than the average (one repeated scalar: 2^20 entries in one or
+// two parts of every window at G1 2^20) was walked twice by its lone workgroup: sort 0.55 ms
+// against 0.13 for random scalars.  k_part_heavy_count plans helpers for such parts from
+// part_tot (every workgroup derives the same plan, part_plan): a part above max(PH_MIN, 4 x the
+// average) entries is heavy and gets ceil(tot / Q) helpers, Q = max(PH_QMIN, heavy entries /
+// (PH_HELPERS - heavy parts)), so at most PH_HELPERS in all; helper i of H takes the part's
+// segments [S i / H, S (i + 1) / H) and counts their fine keys into hh[helper].  k_part_sort then
+// takes a heavy part's fine counts as the sum of its helpers' (its own workgroup: offsets, counts,
+// chunk counts, no walk), and its PH_HELPERS extra workgroups place their ranges: part base +
+// fine prefix + the earlier helpers' counts of the key + LDS rank.  Without a heavy part (random
+// scalars) every helper exits after the plan.  MBLS_PS_HELP=0 builds without them (A/B).
+#ifndef MBLS_PS_HELP
+#define MBLS_PS_HELP 1
+#endif
+static constexpr uint32_t PH_MIN = 32768, PH_QMIN = 8192;
+
+// fn(p, first, H) for every part p < M in order per thread (H = 0: light); all PS_THREADS threads
+template <class Fn>
+MBLS_DEV void part_plan(const uint32_t* __restrict__ part_tot, uint32_t M, Fn&& fn) {
+    constexpr uint32_t NWV = PS_THREADS / 64;
+    __shared__ uint32_t red[4][NWV];
+    const uint32_t per = (M + PS_THREADS - 1) / PS_THREADS;
+    const uint32_t p0 = min(threadIdx.x * per, M), p1 = min(p0 + per, M), wv = threadIdx.x >> 6;
+    auto bsum = [&](uint32_t v, uint32_t* r) {
+        for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+        if ((threadIdx.x & 63) == 0) r[wv] = v;
+        __syncthreads();
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < NWV; ++k) t += r[k];
+        return t;
+    };
+    uint32_t a = 0;
+    for (uint32_t p = p0; p < p1; ++p) a += part_tot[p];
+    const uint32_t total = bsum(a, red[0]);
+    const uint32_t thr = max(PH_MIN, (uint32_t)(4ull * total / M));
+    uint32_t nh = 0, hs = 0;
+    for (uint32_t p = p0; p < p1; ++p) {
+        const uint32_t t = part_tot[p];
+        if (t > thr) ++nh, hs += t;
+    }
+    nh = bsum(nh, red[1]);
+    hs = bsum(hs, red[2]);
+    // many heavy parts already spread over many workgroups: no helpers
+    const bool on = nh > 0 && nh <= PH_HELPERS / 2;
+    const uint32_t Q = on ? max(PH_QMIN, (uint32_t)(((uint64_t)hs + (PH_HELPERS - nh) - 1) / (PH_HELPERS - nh))) : 1u;
+    auto helpers = [&](uint32_t t) { return on && t > thr ? (t + Q - 1) / Q : 0u; };
+    uint32_t hc = 0;
+    for (uint32_t p = p0; p < p1; ++p) hc += helpers(part_tot[p]);
+    const uint32_t incl = wave_incl_scan(hc);
+    if ((threadIdx.x & 63) == 63) red[3][wv] = incl;
+    __syncthreads();
+    uint32_t first = incl - hc;
+    for (uint32_t k = 0; k < wv; ++k) first += red[3][k];
+    for (uint32_t p = p0; p < p1; ++p) {
+        const uint32_t H = helpers(part_tot[p]);
+        fn(p, first, H);
+        first += H;
+    }
+}
+
+// helper i of H's segment range of a part with S segments
+MBLS_DEV void helper_range(uint32_t S, uint32_t i, uint32_t H, uint32_t& s0, uint32_t& s1) {
+    s0 = (uint32_t)((uint64_t)S * i / H);
+    s1 = (uint32_t)((uint64_t)S * (i + 1) / H);
+}
+
+// grid PH_HELPERS: the plan (help, hpart) and the helpers' fine counts (hh)
+template <bool PACK>
+__global__ __launch_bounds__(PS_THREADS) void k_part_heavy_count(const uint32_t* __restrict__ ent,
+                                                          const uint32_t* __restrict__ seg_off,
+                                                          const uint32_t* __restrict__ seg_cnt,
+                                                          const uint32_t* __restrict__ part_tot, uint32_t tiles, int W,
+                                                          int Wg, int FB, uint32_t NP, PartHelp hp) {
+    __shared__ uint32_t cnt[128], mine[3];
+    const uint32_t M = (uint32_t)Wg * NP, g = blockIdx.x;
+    if (threadIdx.x < 128) cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) mine[0] = ~0u, mine[1] = mine[2] = 0;
+    __syncthreads();
+    part_plan(part_tot, M, [&](uint32_t p, uint32_t first, uint32_t H) {
+        if (p % PH_HELPERS == g) hp.help[p] = H ? (first << 16) | H : 0u;  // each part by one workgroup
+        if (H && g >= first && g < first + H) mine[0] = p, mine[1] = g - first, mine[2] = H;
+    });
+    __syncthreads();
+    const uint32_t p = mine[0], i = mine[1], H = mine[2];
+    if (threadIdx.x == 0) hp.hpart[g] = p;
+    if (p == ~0u) return;  // workgroup-uniform
+    const uint32_t wl = p / NP, part = p % NP;
+    const uint32_t S = ((uint32_t)(W - 1 - (int)wl) / (uint32_t)Wg + 1) * tiles;
+    uint32_t s0, s1;
+    helper_range(S, i, H, s0, s1);
+    // a helper's range is a few segments: the whole workgroup walks each (teams per segment
+    // would leave most lanes idle)
+    for (uint32_t s = s0; s < s1; ++s) {
+        const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
+        const uint32_t k = seg_cnt[seg * NP + part];
+        const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
+        part_walk<PACK, PS_THREADS>(ent, o, k, threadIdx.x, FB, [&](uint32_t fine, uint32_t) { lds_count(cnt, fine); });
+    }
+    __syncthreads();
+    if (threadIdx.x < 128) hp.hh[(size_t)g * 128 + threadIdx.x] = threadIdx.x < (1u << FB) ? cnt[threadIdx.x] : 0u;
+}
+
+// helper workgroup g of k_part_sort (blockIdx >= Wg NP): place its segment range of part p
+template <bool PACK>
+MBLS_DEV void part_help_place(const uint32_t* __restrict__ ent, const uint32_t* __restrict__ seg_off,
+                              const uint32_t* __restrict__ seg_cnt, const uint32_t* __restrict__ part_tot,
+                              uint32_t tiles, int W, int Wg, int FB, uint32_t NP, uint32_t* __restrict__ sorted,
+                              const PartHelp& hp, uint32_t* cnt, uint32_t* pre, uint32_t* wsum) {
+    const uint32_t g = blockIdx.x - (uint32_t)Wg * NP;
+    const uint32_t p = hp.hpart[g];
+    if (p == ~0u) return;  // workgroup-uniform
+    const uint32_t h = hp.help[p], first = h >> 16, H = h & 0xffffu, i = g - first;
+    const uint32_t wl = p / NP, part = p % NP, FBN = 1u << FB;
+    // part base: the entries of the parts before p (the scan order of k_part_sort)
+    uint32_t a = 0;
+    for (uint32_t k = threadIdx.x; k < p; k += PS_THREADS) a += part_tot[k];
+    for (int d = 32; d > 0; d >>= 1) a += __shfl_xor(a, d, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = a;
+    if (threadIdx.x < FBN) {  // the part's fine counts, and those of the helpers before this one
+        uint32_t t = 0, before = 0;
+        for (uint32_t k = 0; k < H; ++k) {
+            const uint32_t v = hp.hh[(size_t)(first + k) * 128 + threadIdx.x];
+            t += v;
+            before += k < i ? v : 0u;
+        }
+        cnt[threadIdx.x] = t;
+        pre[threadIdx.x] = before;
+    }
+    __syncthreads();
+    uint32_t base = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PS_THREADS / 64; ++k) base += wsum[k];
+    if (threadIdx.x < 64) {  // pre[f] += exclusive prefix of the fine counts
+        const uint32_t l = threadIdx.x;
+        const uint32_t h0 = 2 * l < FBN ? cnt[2 * l] : 0u, h1 = 2 * l + 1 < FBN ? cnt[2 * l + 1] : 0u;
+        const uint32_t run = wave_incl_scan(h0 + h1) - (h0 + h1);
+        if (2 * l < FBN) pre[2 * l] += run;
+        if (2 * l + 1 < FBN) pre[2 * l + 1] += run + h0;
+    }
+    __syncthreads();
+    if (threadIdx.x < FBN) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t S = ((uint32_t)(W - 1 - (int)wl) / (uint32_t)Wg + 1) * tiles;
+    uint32_t s0, s1;
+    helper_range(S, i, H, s0, s1);
+    for (uint32_t s = s0; s < s1; ++s) {
+        const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
+        const uint32_t k = seg_cnt[seg * NP + part];
+        const size_t o = (size_t)seg * DT_TILE + seg_off[seg * NP + part];
+        part_walk<PACK, PS_THREADS>(ent, o, k, threadIdx.x, FB, [&](uint32_t fine, uint32_t val) {
+            sorted[base + pre[fine] + lds_rank<MBLS_PS_PEEL>(cnt, fine)] = val;
+        });
+    }
+}
+
 template <bool PACK>
 __global__ __launch_bounds__(PS_THREADS) void k_part_sort(const uint32_t* __restrict__ ent, const uint32_t* __restrict__ seg_off,
                                                    const uint32_t* __restrict__ seg_cnt,
                                                    const uint32_t* __restrict__ part_tot, uint32_t tiles, int W,
                                                    int Wg, uint32_t B, int FB, uint32_t NP,
                                                    uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets,
-                                                   uint32_t* __restrict__ sorted, ChunkCountOut cc) {
+                                                   uint32_t* __restrict__ sorted, ChunkCountOut cc, PartHelp hp) {
     __shared__ uint32_t cnt[128], pre[128], span_sh, chist[ORDER_BINS];
     __shared__ uint32_t ps_stage[PS_STAGE > 0 ? PS_STAGE : 1];
+    constexpr uint32_t NWV = PS_THREADS / 64, PJ = 2048 / PS_THREADS;
+    __shared__ uint32_t wsum[NWV];
     const uint32_t FBN = 1u << FB;
+    if (blockIdx.x >= (uint32_t)Wg * NP) {  // a heavy part's helper (grid Wg NP + PH_HELPERS)
+        if (threadIdx.x < FBN) cnt[threadIdx.x] = 0;
+        part_help_place<PACK>(ent, seg_off, seg_cnt, part_tot, tiles, W, Wg, FB, NP, sorted, hp, cnt, pre, wsum);
+        return;
+    }
+    // a heavy part (k_part_heavy_count): its fine counts are its helpers', which also place it
+    const uint32_t help = hp.help ? hp.help[blockIdx.x] : 0u;
     const uint32_t wl = blockIdx.x / NP, part = blockIdx.x % NP;
     // windows of group wl: wl, wl + Wg, ... < W (precompute factor F > 1), `tiles` segments each
     const uint32_t S = ((uint32_t)(W - 1 - (int)wl) / (uint32_t)Wg + 1) * tiles;
@@ -1486,7 +1652,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_sort(const uint32_t* __rest
     // global memory (MBLS_PS_KEEP=0: both passes walk `ent`); the decision is per team
     const uint32_t nseg = team < S ? (S - team + nteams - 1) / nteams : 0u;
     uint32_t sk[PS_RS], so[PS_RS], e[PS_RS * PS_RK];
-    bool keep = PACK && PS_KEEP && nseg <= PS_RS;
+    bool keep = !help && PACK && PS_KEEP && nseg <= PS_RS;
     if (keep) {
 #pragma unroll
         for (uint32_t j = 0; j < PS_RS; ++j) {
@@ -1514,6 +1680,13 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_sort(const uint32_t* __rest
 #pragma unroll
             for (uint32_t q = 0; q < PS_RK; ++q)
                 if (tl + q * PS_TEAM < sk[j]) atomicAdd(&cnt[FB ? e[j * PS_RK + q] >> (32 - FB) : 0u], 1u);
+    } else if (help) {
+        if (threadIdx.x < FBN) {
+            const uint32_t first = help >> 16, H = help & 0xffffu;
+            uint32_t t = 0;
+            for (uint32_t k = 0; k < H; ++k) t += hp.hh[(size_t)(first + k) * 128 + threadIdx.x];
+            cnt[threadIdx.x] = t;
+        }
     } else {
         for (uint32_t s = team; s < S; s += nteams) {
             const uint32_t seg = (wl + (s / tiles) * (uint32_t)Wg) * tiles + s % tiles;
@@ -1525,8 +1698,6 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_sort(const uint32_t* __rest
     // this part's base: the sum of the part totals before it (blockIdx = wl * NP + part, the
     // scan order); block 0 sums them all for offsets[Wg B].  <= Wg * NP = 2048 words: cheaper
     // than the three launches of a separate scan
-    constexpr uint32_t NWV = PS_THREADS / 64, PJ = 2048 / PS_THREADS;
-    __shared__ uint32_t wsum[NWV];
     {
         const uint32_t lim = blockIdx.x == 0 ? (uint32_t)Wg * NP : blockIdx.x;
         uint32_t a = 0;
@@ -1596,6 +1767,7 @@ __global__ __launch_bounds__(PS_THREADS) void k_part_sort(const uint32_t* __rest
         const uint32_t blk = (uint32_t)(((size_t)wl * B + part * FBN) >> 8), bpg = (cc.m + 255) / 256;
         atomicAdd(&cc.binhist[order_index(blk, threadIdx.x, bpg)], chist[threadIdx.x]);
     }
+    if (help) return;  // workgroup-uniform: the helpers place the entries
     __syncthreads();
     // the part's span of `sorted` is assembled in LDS and written out in order (whole lines),
     // instead of one random 4-byte store per entry; a span larger than the stage (adversarial
@@ -1676,16 +1848,29 @@ bool part_sort_fuses_chunks(const MsmPlan& P) { return part_fine_bits(P.B) == CH
 
 eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint32_t* seg_off, const uint32_t* seg_cnt,
                               const uint32_t* part_tot, uint32_t* counts, uint32_t* offsets, uint32_t* sorted,
-                              const ChunkCountOut& cc, hipStream_t st) {
+                              const ChunkCountOut& cc, hipStream_t st, const PartHelp& hp_in) {
     const PartSortSizes z = part_sort_sizes(P);
     if (cc.nchunks && z.FB != CHUNK_FUSED_SHIFT) return MBLS_INVALID_ARGUMENT;
-    dim3 g((uint32_t)P.Wg * z.NP), b(PS_THREADS);
+    if (z.FB > 7) return MBLS_INVALID_ARGUMENT;  // 128 fine counters per part (cnt, pre, hh rows)
+    const bool help = MBLS_PS_HELP && hp_in.help && hp_in.hh && hp_in.hpart;
+    const PartHelp hp = help ? hp_in : PartHelp();
+    const uint32_t M = (uint32_t)P.Wg * z.NP;
+    dim3 g(M + (help ? PH_HELPERS : 0u)), b(PS_THREADS);
+    if (help) {
+        if (z.pack)
+            hipLaunchKernelGGL(k_part_heavy_count<true>, dim3(PH_HELPERS), b, 0, st, ent, seg_off, seg_cnt, part_tot,
+                               z.tiles, P.W, P.Wg, z.FB, z.NP, hp);
+        else
+            hipLaunchKernelGGL(k_part_heavy_count<false>, dim3(PH_HELPERS), b, 0, st, ent, seg_off, seg_cnt, part_tot,
+                               z.tiles, P.W, P.Wg, z.FB, z.NP, hp);
+        MBLS_TRY(hipGetLastError());
+    }
     if (z.pack)
         hipLaunchKernelGGL(k_part_sort<true>, g, b, 0, st, ent, seg_off, seg_cnt, part_tot, z.tiles, P.W, P.Wg, P.B,
-                           z.FB, z.NP, counts, offsets, sorted, cc);
+                           z.FB, z.NP, counts, offsets, sorted, cc, hp);
     else
         hipLaunchKernelGGL(k_part_sort<false>, g, b, 0, st, ent, seg_off, seg_cnt, part_tot, z.tiles, P.W, P.Wg, P.B,
-                           z.FB, z.NP, counts, offsets, sorted, cc);
+                           z.FB, z.NP, counts, offsets, sorted, cc, hp);
     MBLS_TRY(hipGetLastError());
     return MBLS_SUCCESS;
 }

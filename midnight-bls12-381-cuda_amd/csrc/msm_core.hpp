@@ -167,6 +167,15 @@ struct ChunkCountOut {
 };
 static constexpr int CHUNK_FUSED_SHIFT = 7;
 bool part_sort_fuses_chunks(const MsmPlan& P);
+// helpers of heavy parts (skewed scalars; msm_common.hip k_part_heavy_count): help[M] per part
+// (first helper << 16 | helpers, 0: light), hh[PH_HELPERS][128] the helpers' fine counts,
+// hpart[PH_HELPERS] each helper's part (~0: idle)
+static constexpr uint32_t PH_HELPERS = 512;
+struct PartHelp {
+    uint32_t* help = nullptr;
+    uint32_t* hh = nullptr;
+    uint32_t* hpart = nullptr;
+};
 // zero2 / nzero2: words the digit pass clears besides its own (the fused order histograms)
 eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, const MsmPlan& P, uint32_t* ent,
                                 uint32_t* seg_off, uint32_t* seg_cnt, uint32_t* part_tot, uint8_t* dsrc,
@@ -175,7 +184,7 @@ eIcicleError launch_digits_part(const uint8_t* scalars, bool mont, uint32_t n, c
 // counts: the bucket counts, or with cc.nchunks the chunk-count prefixes (cloc)
 eIcicleError launch_part_sort(const MsmPlan& P, const uint32_t* ent, const uint32_t* seg_off, const uint32_t* seg_cnt,
                               const uint32_t* part_tot, uint32_t* counts, uint32_t* offsets, uint32_t* sorted,
-                              const ChunkCountOut& cc, hipStream_t st);
+                              const ChunkCountOut& cc, hipStream_t st, const PartHelp& hp = PartHelp());
 
 // ------------------------------------------------------------------------------------
 // 4. accumulation: thread t sums the L contributions at sorted positions [L t, L t + L),
@@ -991,9 +1000,10 @@ struct MsmScratchSizes {
     size_t ent, segtab, parts;  // partitioned sort (keys / vals / ranks are 0 then)
     size_t order, perm;         // k_bucket_order: bin histograms / their scan, bucket permutation
     size_t heavy, hslices, hres;  // HeavyTab: per-entry words (x4), per-slice owner words, slice sums
+    size_t phelp;                 // PartHelp: hh + hpart (help shares the second `parts` array)
     size_t total() const {
         return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + first + partials + buckets + levelT + levelR +
-               windows + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm + 4 * heavy + hslices + hres;
+               windows + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm + 4 * heavy + hslices + hres + phelp;
     }
 };
 
@@ -1023,7 +1033,9 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
         z.ent = align_up(s.ent);
         z.segtab = align_up(s.segtab);
         z.parts = align_up(s.parts);
+        z.phelp = align_up((size_t)PH_HELPERS * 129 * 4);
     } else {
+        z.phelp = 0;
         z.keys = align_up(NC * 4);
         z.vals = align_up(NC * 4);
         z.ranks = align_up(NC * 4);
@@ -1199,7 +1211,10 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     uint32_t* seg_off = (uint32_t*)arena.take(z.segtab);
     uint32_t* seg_cnt = (uint32_t*)arena.take(z.segtab);
     uint32_t* part_tot = (uint32_t*)arena.take(z.parts);
-    uint32_t* part_base = (uint32_t*)arena.take(z.parts);
+    PartHelp ph;
+    ph.help = (uint32_t*)arena.take(z.parts);
+    ph.hh = (uint32_t*)arena.take(z.phelp);
+    ph.hpart = ph.hh ? ph.hh + (size_t)PH_HELPERS * 128 : nullptr;
     uint32_t* binhist = (uint32_t*)arena.take(z.order);
     uint32_t* binbase = (uint32_t*)arena.take(z.order);
     uint32_t* perm = (uint32_t*)arena.take(z.perm);
@@ -1211,7 +1226,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     H.owner = (uint32_t*)arena.take(z.hslices);
     H.res = (uint8_t*)arena.take(z.hres);
     H.cnt = nchunks + TB + 1;
-    if (!H.res || !windows || (img_table && !phi) || !part_base) return MBLS_ALLOCATION_FAILED;
+    if (!H.res || !windows || (img_table && !phi) || (psort && !ph.hh)) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
@@ -1270,7 +1285,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
                 cc.L = P.chunk;
                 cc.m = TB;
             }
-            er = launch_part_sort(P, ent, seg_off, seg_cnt, part_tot, counts, offsets, sorted, cc, st);
+            er = launch_part_sort(P, ent, seg_off, seg_cnt, part_tot, counts, offsets, sorted, cc, st, ph);
             if (er != MBLS_SUCCESS) return er;
         } else if ((er = scan_exclusive(counts, offsets, TB, tmp, st)) != MBLS_SUCCESS) {
             return er;
