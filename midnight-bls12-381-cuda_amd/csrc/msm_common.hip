@@ -1083,15 +1083,7 @@ eIcicleError launch_digits(const uint8_t* scalars, bool mont, uint32_t n, const 
 // ------------------------------------------------------------------------------------
 // 2. exclusive scan: three phases, 1024 elements per block, wave64 shuffles
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
+// (wave_incl_scan: msm_core.hpp)
 
 __device__ __forceinline__ void block_scan_1024(uint32_t (&x)[4], uint32_t* sh_wave, uint32_t& total) {
     uint32_t s0 = x[0], s1 = s0 + x[1], s2 = s1 + x[2], s3 = s2 + x[3];
@@ -2070,6 +2062,8 @@ __global__ __launch_bounds__(256) void k_chunk_owner(const uint32_t* __restrict_
         for (uint32_t k = qk0[q] + threadIdx.x; k < qk1[q]; k += blockDim.x) owner[k] = qv;
         for (uint32_t t = qt0[q] + threadIdx.x; t < qt1[q]; t += blockDim.x) first[t] = qv;
     }
+    if (blockIdx.x == 0)  // the planned slices' group counters (heavy_slices)
+        for (uint32_t i = threadIdx.x; i < HEAVY_GDONE; i += blockDim.x) H.gdone[i] = 0;
     if (b >= m) return;
     const uint32_t c = nchunks[b];
     if (c <= SMALL_MAX) {

@@ -50,6 +50,9 @@ static constexpr uint32_t INVALID_KEY = 0xffffffffu;
 #define MBLS_SETPRIO 3
 #endif
 #define MBLS_TAIL_PRIO() __builtin_amdgcn_s_setprio(MBLS_SETPRIO)
+#ifndef MBLS_LIGHT_PRIO
+#define MBLS_LIGHT_PRIO 2
+#endif
 #ifndef MBLS_CHUNK
 #define MBLS_CHUNK 16
 #endif
@@ -131,7 +134,9 @@ struct HeavyTab {
     uint32_t* done;     // entry e -> slices finished (last-block-done counter)
     uint32_t* owner;    // slice g -> its entry
     uint8_t* res;       // slice g -> its sum (Jacobian)
+    uint32_t* gdone;    // planned slices: group of HEAVY_GROUP slices led by g -> slices finished
 };
+static constexpr uint32_t HEAVY_GDONE = 2048;  // gdone words (zeroed by k_chunk_owner)
 // cloc / blk_pre: the chunk-count prefixes inside blocks of 2^cs buckets and the blocks' scan
 eIcicleError launch_chunk_owner(const uint32_t* cloc, const uint32_t* blk_pre, int cs, uint32_t* chunk_off,
                                 const uint32_t* offsets, uint32_t m, uint32_t L, uint32_t* owner, uint32_t* first,
@@ -514,7 +519,7 @@ constexpr uint32_t lanes_per_chain() { return MODE == MODE_LANE ? 1u : MODE == M
 // ------------------------------------------------------------------------------------
 // 5. bucket sums from chunk partials.  Light buckets (<= SMALL_MAX partials -- every bucket of
 //    random inputs): one thread each.  Heavy buckets (equal scalars, adversarial inputs): cut into
-//    slices of HEAVY_SLICE partials, listed by k_chunk_owner (HeavyTab); one workgroup per slice
+//    slices (heavy_slices' plan, or HEAVY_SLICE partials listed by k_chunk_owner); one workgroup per slice
 //    sums its slice (strided chains + an LDS tree), and the workgroup that finishes a bucket's
 //    last slice (a counter per bucket: last-block-done) sums the bucket's slice sums.  The slice
 //    workgroups ride in the same launch as the light buckets (HEAVY_BLOCKS extra workgroups that
@@ -554,11 +559,57 @@ MBLS_DEV RJac<F> rows_sum_chains(uint8_t* sh, uint32_t chains) {
     using IO = RedIO<F, MODE_ROW>;
     constexpr uint32_t ROWS = 256 / 16;
     const uint32_t r = threadIdx.x >> 4;
-    RJac<F> acc = RJac<F>::inf();
-    for (uint32_t k = r; k < chains; k += ROWS) acc = IO::add(acc, IO::ld(sh, k));
+    RJac<F> acc = r < chains ? IO::ld(sh, r) : RJac<F>::inf();  // no addition to the identity first
+    for (uint32_t k = r + ROWS; k < chains; k += ROWS) acc = IO::add(acc, IO::ld(sh, k));
     // row r has read its slots (k = r, r + 16, ...); row_tree overwrites only slot r < 16
     return row_tree<F>(acc, sh, r);
 }
+
+// inclusive wave64 scan (shuffles)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// r28 lane addition of chunk partial k (G1: the light path's and the slice chains' form)
+MBLS_DEV void r28_add_partial(r28::J28& acc, const uint8_t* __restrict__ partials, uint32_t k) {
+    const uint4* q = reinterpret_cast<const uint4*>(partials + (size_t)k * 144);
+    uint32_t w[3][12], zany = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint4 u = q[3 * c + j];
+            w[c][4 * j] = u.x, w[c][4 * j + 1] = u.y, w[c][4 * j + 2] = u.z, w[c][4 * j + 3] = u.w;
+        }
+#pragma unroll
+    for (int j = 0; j < 12; ++j) zany |= w[2][j];
+    if (zany) r28::jadd(acc, r28::unpack_shift8(w[0]), r28::unpack_shift8(w[1]), r28::unpack_shift8(w[2]));
+}
+
+// Slice plan (round 5): the slice length S adapts to the heavy partials T of the call, S =
+// clamp(pow2 >= T / (slice workgroups), HEAVY_SLICE_MIN, HEAVY_SLICE), so that few heavy buckets
+// (half the scalars 1: one bucket of 2^15 partials at G1 2^20) spread over many workgroups
+// instead of 16 slices of 8-deep lane chains, while many (one repeated scalar: 16 buckets of 2^16)
+// keep 2048-partial slices, one round of workgroups.  Every slice workgroup derives the plan from
+// the heavy-bucket list (their chunk counts, a prefix of slices per bucket in LDS); more than
+// HEAVY_LDS heavy buckets take k_chunk_owner's fixed HEAVY_SLICE plan (H.owner / first / nslices).
+// Planned slices finish in groups of HEAVY_GROUP: the workgroup finishing a group's last slice
+// sums the group (one row each, a 4-level row tree), the one finishing a bucket's last group sums
+// the group sums -- with 64-partial slices a bucket of 2^15 partials takes 3 + 4, 4 and 2 + 4
+// dependent row additions instead of 16 + 4 and 32 + 4 in one level.
+#ifndef MBLS_HEAVY_SLICE_MIN
+#define MBLS_HEAVY_SLICE_MIN 256
+#endif
+#ifndef MBLS_HEAVY_TRACE
+#define MBLS_HEAVY_TRACE 0
+#endif
+static constexpr uint32_t HEAVY_SLICE_MIN = MBLS_HEAVY_SLICE_MIN, HEAVY_LDS = 1024, HEAVY_GROUP = 16;
 
 template <class F>
 MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ partials,
@@ -568,39 +619,140 @@ MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t
     constexpr uint32_t LN = LaneOf<F>::LANES;
     constexpr uint32_t CHAINS = 256 / LN;
     __shared__ __attribute__((aligned(16))) uint8_t sh[CHAINS * 3 * sizeof(F)];
-    __shared__ uint32_t last;
-    const uint32_t nsl = H.cnt[1];
+    __shared__ uint32_t last, hfirst[HEAVY_LDS + 1], wred[4];
+    const uint32_t nh = H.cnt[0];
+    if (nh == 0) return;  // workgroup-uniform (random scalars: every slice workgroup leaves here)
+#if MBLS_HEAVY_TRACE  // diagnostic builds only: per-workgroup wall-clock stamps
+    const uint64_t tr0 = wall_clock64();
+    uint64_t trs = 0, trg = 0;
+#endif
+    const bool planned = nh <= HEAVY_LDS;
+    uint32_t S = HEAVY_SLICE, nsl = H.cnt[1];
+    if (planned) {
+        const uint32_t per = (nh + 255) / 256, e0 = min(threadIdx.x * per, nh), e1 = min(e0 + per, nh);
+        uint32_t t = 0;
+        for (uint32_t e = e0; e < e1; ++e) {
+            const uint32_t b = H.bucket[e];
+            t += chunk_off[b + 1] - chunk_off[b];
+        }
+        uint32_t r = t;
+        for (int d = 32; d > 0; d >>= 1) r += __shfl_xor(r, d, 64);
+        if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6] = r;
+        __syncthreads();
+        const uint32_t T = wred[0] + wred[1] + wred[2] + wred[3];
+        const uint32_t want = (T + nhb - 1) / nhb;
+        S = HEAVY_SLICE_MIN;
+        while (S < want && S < HEAVY_SLICE) S <<= 1;
+        uint32_t c = 0;
+        for (uint32_t e = e0; e < e1; ++e) {
+            const uint32_t b = H.bucket[e];
+            c += (chunk_off[b + 1] - chunk_off[b] + S - 1) / S;
+        }
+        const uint32_t incl = wave_incl_scan(c);
+        __syncthreads();  // wred is reused
+        if ((threadIdx.x & 63) == 63) wred[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        uint32_t f = incl - c;
+        for (uint32_t k = 0; k < (threadIdx.x >> 6); ++k) f += wred[k];
+        for (uint32_t e = e0; e < e1; ++e) {
+            const uint32_t b = H.bucket[e];
+            hfirst[e] = f;
+            f += (chunk_off[b + 1] - chunk_off[b] + S - 1) / S;
+        }
+        if (e1 == nh && e0 < e1) hfirst[nh] = f;
+        __syncthreads();
+        nsl = hfirst[nh];
+    }
+    // slices <= nhb + nh with S >= T / nhb: within HEAVY_GDONE for nh <= HEAVY_LDS (checked anyway)
+    const bool grouped = planned && nsl <= HEAVY_GDONE;
     const uint32_t j = threadIdx.x / LN;
     for (uint32_t g = hb; g < nsl; g += nhb) {
-        const uint32_t e = H.owner[g], b = H.bucket[e];
-        const uint32_t c0 = chunk_off[b] + (g - H.first[e]) * HEAVY_SLICE;
-        const uint32_t c1 = min(c0 + HEAVY_SLICE, chunk_off[b + 1]);
-        Jacobian<L> acc = Jacobian<L>::inf();
-        for (uint32_t k = c0 + j; k < c1; k += CHAINS) acc = jac_add(acc, load_jac<L>(partials, k));
-        store_jac<L>(sh, j, acc);
+        uint32_t e, f0, ns;
+        if (planned) {  // the bucket whose slices hold g: last e with hfirst[e] <= g
+            uint32_t lo = 0, hi = nh;  // hfirst[lo] <= g < hfirst[hi]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (hfirst[mid] <= g)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            e = lo, f0 = hfirst[lo], ns = hfirst[lo + 1] - f0;
+        } else {
+            e = H.owner[g], f0 = H.first[e], ns = H.nslices[e];
+        }
+        const uint32_t b = H.bucket[e];
+        const uint32_t c0 = chunk_off[b] + (g - f0) * S;
+        const uint32_t c1 = min(c0 + S, chunk_off[b + 1]);
+        if constexpr (std::is_same<L, Fq>::value && MBLS_BS_R28) {
+            r28::J28 acc = r28::J28::inf();
+            for (uint32_t k = c0 + j; k < c1; k += CHAINS) r28_add_partial(acc, partials, k);
+            store_jac28(sh, j, acc);
+        } else {
+            Jacobian<L> acc = Jacobian<L>::inf();
+            for (uint32_t k = c0 + j; k < c1; k += CHAINS) acc = jac_add(acc, load_jac<L>(partials, k));
+            store_jac<L>(sh, j, acc);
+        }
         __syncthreads();
-        const RJac<F> ssum = rows_sum_chains<F>(sh, CHAINS);
+        const RJac<F> ssum = rows_sum_chains<F>(sh, min(CHAINS, c1 - c0));
+#if MBLS_HEAVY_TRACE
+        trs = wall_clock64();
+#endif
         if (threadIdx.x < 16) IO::st(H.res, g, ssum);
         __threadfence();
         __syncthreads();
-        if (threadIdx.x == 0) last = atomicAdd(&H.done[e], 1u) + 1 == H.nslices[e] ? 1u : 0u;
-        __syncthreads();
-        if (last) {  // this workgroup finished bucket b's last slice: sum the slice sums
+        const uint32_t r = threadIdx.x >> 4;
+        // the sums to combine at the bucket level: slice sums (one level), or the group sums at
+        // f0, f0 + HEAVY_GROUP, ... (grouped)
+        uint32_t nsum = ns, step = 1;
+        if (grouped) {
+            const uint32_t gl = f0 + (g - f0) / HEAVY_GROUP * HEAVY_GROUP;  // the group's first slice
+            const uint32_t gs = min(HEAVY_GROUP, f0 + ns - gl);
+            if (threadIdx.x == 0) last = atomicAdd(&H.gdone[gl], 1u) + 1 == gs ? 1u : 0u;
+            __syncthreads();
+            if (!last) continue;  // workgroup-uniform; sh and `last` are rewritten after barriers
             __threadfence();
-            const uint32_t ns = H.nslices[e], f0 = H.first[e], r = threadIdx.x >> 4;
-            RJac<F> tot = RJac<F>::inf();
-            for (uint32_t k = r; k < ns; k += 16) tot = IO::add(tot, IO::ld(H.res, f0 + k));
+            RJac<F> gsum = r < gs ? IO::ld(H.res, gl + r) : RJac<F>::inf();
+            gsum = row_tree<F>(gsum, sh, r);
+            if (threadIdx.x < 16) IO::st(H.res, gl, gsum);
+#if MBLS_HEAVY_TRACE
+            trg = wall_clock64();
+#endif
+            __threadfence();
+            __syncthreads();
+            nsum = (ns + HEAVY_GROUP - 1) / HEAVY_GROUP, step = HEAVY_GROUP;
+        }
+        if (threadIdx.x == 0) last = atomicAdd(&H.done[e], 1u) + 1 == nsum ? 1u : 0u;
+        __syncthreads();
+        if (last) {  // this workgroup finished bucket b's last slice (group): sum the sums
+#if MBLS_HEAVY_TRACE
+            const uint64_t trf0 = wall_clock64();
+#endif
+            __threadfence();
+#if MBLS_HEAVY_TRACE
+            const uint64_t trf1 = wall_clock64();
+#endif
+            RJac<F> tot = r < nsum ? IO::ld(H.res, f0 + r * step) : RJac<F>::inf();
+            for (uint32_t k = r + 16; k < nsum; k += 16) tot = IO::add(tot, IO::ld(H.res, f0 + k * step));
             tot = row_tree<F>(tot, sh, r);
             if (threadIdx.x < 16) IO::st(buckets, b, tot);
+#if MBLS_HEAVY_TRACE
+            const uint64_t trb = wall_clock64();
+            if (threadIdx.x == 0)
+                printf("HB g=%u e=%u t0=%llu ts=%llu tg=%llu tf0=%llu tf1=%llu tb=%llu\n", g, e, tr0, trs, trg, trf0, trf1, trb);
+#endif
         }
+#if MBLS_HEAVY_TRACE
+        else if (threadIdx.x == 0) printf("HS g=%u e=%u t0=%llu ts=%llu tg=%llu\n", g, e, tr0, trs, trg);
+#endif
         __syncthreads();  // sh and `last` are reused by the next slice
     }
 }
 
 // light buckets: one thread per bucket (<= SMALL_MAX chunks) sums its chunk partials; thread t
 // takes perm[start + t] (k_chunk_owner: buckets grouped by chunk count, heaviest first, so a
-// wave's lanes run the same number of additions).  Workgroups from `light_blocks` on take the
-// heavy slices.
+// wave's lanes run the same number of additions).  The first HEAVY_BLOCKS workgroups take the
+// heavy slices, the light buckets' `light_blocks` follow.
 template <class F>
 // 2 waves per SIMD: G1 fits anyway (181 VGPRs); G2's pair-sliced sums took 260 VGPRs + 4 AGPRs,
 // i.e. one latency-bound wave per SIMD -- capped at 256 (4 spilled) its bucket sums take 0.93
@@ -614,32 +766,25 @@ __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32
                                                       uint8_t* __restrict__ buckets, uint32_t light_blocks, HeavyTab H) {
     MBLS_TAIL_PRIO();
     using L = typename LaneOf<F>::type;
-    if (blockIdx.x >= light_blocks) {
-        heavy_slices<F>(chunk_off, partials, buckets, H, blockIdx.x - light_blocks, gridDim.x - light_blocks);
+    // the slice workgroups come first: dispatched at once, the heavy buckets' chains overlap the
+    // light buckets (they used to start behind them: G1 2^20 half ones ~0.1 ms)
+    if (blockIdx.x < HEAVY_BLOCKS) {
+        heavy_slices<F>(chunk_off, partials, buckets, H, blockIdx.x, HEAVY_BLOCKS);
         return;
     }
+    // light workgroups one wave-priority step below the slice workgroups: the heavy buckets'
+    // dependent row chains share CUs with them (G1 2^20 half ones: a bucket-level row tree took
+    // 130-220 us beside light sums instead of ~45)
+    __builtin_amdgcn_s_setprio(MBLS_LIGHT_PRIO);
     const uint32_t start = binbase[0], stop = binbase[gwords];
-    const uint32_t t = start + (blockIdx.x * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
+    const uint32_t t = start + ((blockIdx.x - HEAVY_BLOCKS) * blockDim.x + threadIdx.x) / LaneOf<F>::LANES;
     if (t >= stop) return;
     const uint32_t b = perm[t];
     const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
     if constexpr (std::is_same<L, Fq>::value && MBLS_BS_R28) {
         // radix 2^28 (mbls_fq28.hpp jadd; same values as jac_add, round 5)
         r28::J28 acc = r28::J28::inf();
-        for (uint32_t k = k0; k < k1; ++k) {
-            const uint4* q = reinterpret_cast<const uint4*>(partials + (size_t)k * 144);
-            uint32_t w[3][12], zany = 0;
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    const uint4 u = q[3 * c + j];
-                    w[c][4 * j] = u.x, w[c][4 * j + 1] = u.y, w[c][4 * j + 2] = u.z, w[c][4 * j + 3] = u.w;
-                }
-#pragma unroll
-            for (int j = 0; j < 12; ++j) zany |= w[2][j];
-            if (zany) r28::jadd(acc, r28::unpack_shift8(w[0]), r28::unpack_shift8(w[1]), r28::unpack_shift8(w[2]));
-        }
+        for (uint32_t k = k0; k < k1; ++k) r28_add_partial(acc, partials, k);
         store_jac28(buckets, b, acc);
         return;
     }
@@ -1001,9 +1146,10 @@ struct MsmScratchSizes {
     size_t order, perm;         // k_bucket_order: bin histograms / their scan, bucket permutation
     size_t heavy, hslices, hres;  // HeavyTab: per-entry words (x4), per-slice owner words, slice sums
     size_t phelp;                 // PartHelp: hh + hpart (help shares the second `parts` array)
+    size_t gdone = align_up(HEAVY_GDONE * 4);
     size_t total() const {
         return dsrc + keys + vals + ranks + sorted + 4 * words + tmp + owner + first + partials + buckets + levelT + levelR +
-               windows + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm + 4 * heavy + hslices + hres + phelp;
+               windows + phi + ent + 2 * segtab + 2 * parts + 2 * order + perm + 4 * heavy + hslices + hres + phelp + gdone;
     }
 };
 
@@ -1050,7 +1196,9 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     const size_t max_slices = max_chunks / HEAVY_SLICE + max_heavy + 1;
     z.heavy = align_up(max_heavy * 4);
     z.hslices = align_up(max_slices * 4);
-    z.hres = align_up(max_slices * jac);
+    // slice sums: the planned slices (>= HEAVY_SLICE_MIN partials, <= HEAVY_LDS buckets) or the
+    // fixed plan's
+    z.hres = align_up(std::max(max_slices, max_chunks / HEAVY_SLICE_MIN + std::min<size_t>(max_heavy, HEAVY_LDS) + 1) * jac);
     z.order = align_up(((size_t)order_words(P.TB) + 1) * 4);
     z.perm = align_up((size_t)P.TB * 4);
     // + the chunk-count block totals and their prefixes (k_chunk_counts / k_scan_small)
@@ -1225,8 +1373,9 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     H.done = (uint32_t*)arena.take(z.heavy);
     H.owner = (uint32_t*)arena.take(z.hslices);
     H.res = (uint8_t*)arena.take(z.hres);
+    H.gdone = (uint32_t*)arena.take(z.gdone);
     H.cnt = nchunks + TB + 1;
-    if (!H.res || !windows || (img_table && !phi) || (psort && !ph.hh)) return MBLS_ALLOCATION_FAILED;
+    if (!H.gdone || !H.res || !windows || (img_table && !phi) || (psort && !ph.hh)) return MBLS_ALLOCATION_FAILED;
 
     ProfScope prof_all("msm.total", st);
     eIcicleError er;
