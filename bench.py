@@ -38,7 +38,7 @@ PROFILES = os.path.join(ROOT, "profiles")
 
 
 def pmc_summary():
-    for rnd in ("r04/closing", "r03", "r02", "r01"):
+    for rnd in ("r05/closing", "r04/closing", "r03", "r02", "r01"):
         path = os.path.join(PROFILES, rnd, "pmc_summary.json")
         try:
             with open(path) as f:
@@ -380,7 +380,9 @@ def main():
         ntt_ach = NTT_BYTES_PER_ELEM * nn / (ntt_ms * 1e-3) / 1e9 if ntt_ms else None
         _, pmc_src = pmc_summary()
         ceil = valu_ceiling() or {}
-        acc_c, ntt_c = ceil.get("acc_ceiling") or {}, ceil.get("ntt_ceiling") or {}
+        # G1's accumulation is k_accumulate_r28 (round 5): its own arithmetic's ceiling when measured
+        acc_c = ceil.get("acc28_ceiling") or ceil.get("acc_ceiling") or {}
+        ntt_c = ceil.get("ntt_ceiling") or {}
         isa = ceil.get("isa_2") or {}
         cyc = isa.get("simd_cycles_per_wave_instr")
         # the ceiling's ns per contribution at this MSM's contribution count
@@ -436,8 +438,8 @@ def main():
                               "counter_issue_ms": round(acc_issue, 4) if acc_issue else None,
                               "counter_issue_frac": round(acc_issue / acc_ms, 4) if acc_issue and acc_ms else None,
                               "counter_source": f"{pmc_src} (SQ_INSTS_VALU per launch)" if pmc_src else None,
-                              "note": f"{contributions} mixed additions per launch; peak = k_acc_ceiling "
-                                      "(tools/valu_ceiling.hip: the same madd / mmadd code, launch bounds and chunk "
+                              "note": f"{contributions} mixed additions per launch; peak = k_acc28_ceiling "
+                                      "(tools/valu_ceiling.hip: the same radix-2^28 madd / mmadd code, launch bounds and chunk "
                                       "structure with the points in LDS: no random gathers), measured on the box; "
                                       "frac = ceiling time / kernel time.  counter_issue_ms = the committed VALU "
                                       "instruction count at the measured cycles per wave-instruction and clock"},

@@ -1054,12 +1054,21 @@ template <class F>
 __global__ __launch_bounds__(64) void k_final_icicle(const uint8_t* __restrict__ windows, int Wg, int c,
                                                      uint8_t* __restrict__ out) {
     MBLS_TAIL_PRIO();
+#if MBLS_HEAVY_TRACE
+    const uint64_t t0 = wall_clock64();
+#endif
     const RJac<F> acc = final_fold<F, MODE_WAVE>(windows, Wg, c);
     Jacobian<F> p;
     p.x = row_to_lane(acc.x);
     p.y = row_to_lane(acc.y);
     p.z = row_to_lane(acc.z);
+#if MBLS_HEAVY_TRACE
+    const uint64_t t1 = wall_clock64();
+#endif
     if (threadIdx.x == 0) icicle_point<F>(p, out, 0);
+#if MBLS_HEAVY_TRACE
+    if (threadIdx.x == 0) printf("FIN fold=%llu inv=%llu\n", t1 - t0, wall_clock64() - t1);
+#endif
 }
 
 template <class F>

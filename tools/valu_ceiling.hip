@@ -26,6 +26,7 @@
 #include <vector>
 #include "mbls_curve.hpp"
 #include "mbls_fips.hpp"
+#include "mbls_fq28.hpp"
 
 #define CK(x)                                                                        \
     do {                                                                             \
@@ -118,6 +119,80 @@ __global__ __launch_bounds__(256, 3) void k_acc_ceiling(const uint8_t* __restric
             if (!done) acc = jac_madd(acc, q);
         }
         store_jac<Fq>(partials, (size_t)tid * chunks_per_thread + ch, acc);
+    }
+    clk_end(rec, c0, w0);
+}
+
+// k_accumulate_r28's arithmetic (round 5: unsaturated radix-2^28 Fq, mbls_fq28.hpp): the same
+// madd / mmadd with acc.y parked in a per-lane LDS slot across the addition's middle (the kernel
+// parks it in its free stage slot), same launch bounds
+struct ParkLds {
+    uint4* q;  // this lane's 4 pieces, stride 256
+    r28::F28 x;
+    MBLS_DEV void put(int s, const r28::F28& a) {
+        if (s == 0) {
+            x = a;
+            return;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            q[256 * k] = make_uint4(a.l[4 * k], a.l[4 * k + 1], k < 3 ? a.l[4 * k + 2] : 0u, k < 3 ? a.l[4 * k + 3] : 0u);
+        asm volatile("" ::: "memory");
+    }
+    MBLS_DEV r28::F28 get(int s) const {
+        if (s == 0) return x;
+        asm volatile("" ::: "memory");
+        r28::F28 r;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 u = q[256 * k];
+            r.l[4 * k] = u.x;
+            r.l[4 * k + 1] = u.y;
+            if (k < 3) {
+                r.l[4 * k + 2] = u.z;
+                r.l[4 * k + 3] = u.w;
+            }
+        }
+        return r;
+    }
+};
+
+template <int CHUNK>
+__global__ __launch_bounds__(256, 3) void k_acc28_ceiling(const uint8_t* __restrict__ table, uint8_t* __restrict__ partials,
+                                                          Clk* rec, uint32_t chunks_per_thread, uint32_t seed) {
+    unsigned long long c0, w0;
+    clk_begin(c0, w0);
+    __shared__ uint4 pts[PTS * 6];
+    __shared__ uint4 park[4 * 256];
+    for (int k = threadIdx.x; k < PTS * 6; k += blockDim.x) pts[k] = reinterpret_cast<const uint4*>(table)[k];
+    __syncthreads();
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t h = seed ^ (tid * 0x9e3779b9u);
+    for (uint32_t ch = 0; ch < chunks_per_thread; ++ch) {
+        r28::J28 acc = r28::J28::inf();
+        for (int e = 0; e < CHUNK; ++e) {
+            h = h * 1664525u + 1013904223u;
+            const uint32_t idx = (h >> 8) & (PTS - 1);
+            uint32_t xw[12], yw[12];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint4 xa = pts[idx * 6 + k], ya = pts[idx * 6 + 3 + k];
+                xw[4 * k] = xa.x, xw[4 * k + 1] = xa.y, xw[4 * k + 2] = xa.z, xw[4 * k + 3] = xa.w;
+                yw[4 * k] = ya.x, yw[4 * k + 1] = ya.y, yw[4 * k + 2] = ya.z, yw[4 * k + 3] = ya.w;
+            }
+            const r28::F28 qx = r28::unpack_shift8(xw);
+            r28::F28 qy = r28::unpack_shift8(yw);
+            if (h & 1) qy = r28::neg<r28::B512>(qy);
+            bool done = false;
+            if (e == 1 && !acc.is_inf()) done = r28::mmadd(acc, qx, qy);
+            ParkLds pk{&park[threadIdx.x]};
+            if (!done) r28::madd(acc, qx, qy, pk);
+        }
+        Jacobian<Fq> out;
+        r28::to_words(acc.x, out.x.v);
+        r28::to_words(acc.y, out.y.v);
+        r28::to_words(acc.z, out.z.v);
+        store_jac<Fq>(partials, (size_t)tid * chunks_per_thread + ch, out);
     }
     clk_end(rec, c0, w0);
 }
@@ -277,6 +352,15 @@ int main(int argc, char** argv) {
                "\"contributions\": %.0f, \"ms\": %.4f, \"ns_per_contribution_chip\": %.6f, \"mhz_med\": %.0f, "
                "\"mhz_min\": %.0f, \"mhz_max\": %.0f, \"ms_per_2^20_g1_msm_contributions\": %.4f}",
                done, t.ms, t.ms * 1e6 / done, t.mhz_med, t.mhz_min, t.mhz_max, t.ms / done * 16777216.0);
+        auto L28 = [&] {
+            hipLaunchKernelGGL(k_acc28_ceiling<16>, dim3(threads / 256), dim3(256), 0, 0, d_tab, d_part, d_rec, per, 99u);
+        };
+        Timing t28 = run(L28, d_rec, threads / 64, 5);
+        printf(",\n \"acc28_ceiling\": {\"kernel\": \"k_acc28_ceiling<16> (k_accumulate_r28 arithmetic: radix-2^28 Fq, "
+               "acc.y parked in LDS; points from LDS)\", "
+               "\"contributions\": %.0f, \"ms\": %.4f, \"ns_per_contribution_chip\": %.6f, \"mhz_med\": %.0f, "
+               "\"mhz_min\": %.0f, \"mhz_max\": %.0f, \"ms_per_2^20_g1_msm_contributions\": %.4f}",
+               done, t28.ms, t28.ms * 1e6 / done, t28.mhz_med, t28.mhz_min, t28.mhz_max, t28.ms / done * 16777216.0);
         CK(hipFree(d_tab));
         CK(hipFree(d_part));
     }
