@@ -799,17 +799,22 @@ def _skewed(case, n, g):
         return [1 << (i % 63) for i in range(n)]
     if case == "repeated":
         return [g.randrange(pr.R)] * n
+    if case == "few_values":  # 2048 distinct values: thousands of heavy buckets (the fixed slice plan)
+        pool = [g.randrange(pr.R) for _ in range(2048)]
+        return [pool[g.randrange(2048)] for _ in range(n)]
     raise ValueError(case)
 
 
 @pytest.mark.parametrize("group,log_n,case", [("g1", 15, "ones"), ("g1", 15, "half_one"), ("g1", 15, "bits8"),
                                               ("g1", 15, "bit_of_64"), ("g1", 15, "repeated"), ("g1", 20, "ones"),
-                                              ("g1", 20, "half_one"), ("g1", 22, "ones"), ("g2", 14, "ones"),
-                                              ("g2", 14, "bits8"),
-                                              ("g2", 14, "repeated")])
+                                              ("g1", 20, "half_one"), ("g1", 20, "repeated"), ("g1", 20, "few_values"),
+                                              ("g1", 22, "ones"), ("g2", 14, "ones"), ("g2", 14, "bits8"),
+                                              ("g2", 14, "repeated"), ("g2", 16, "repeated"), ("g2", 16, "half_one")])
 def test_msm_skewed_scalars(amd, gh, group, log_n, case):
     """skewed scalar distributions put most contributions into a few buckets (heavy parts of the
-    partitioned sort, long owner ranges, heavy bucket slices) -- equal to the oracle"""
+    partitioned sort and their helper workgroups -- parts above 2^15 entries: G1 2^20, G2 2^16 --,
+    long owner ranges, heavy bucket slices: planned and grouped, or the fixed plan past 1024 heavy
+    buckets with `few_values`) -- equal to the oracle"""
     import torch
     n = 1 << log_n
     w = 12 if group == "g1" else 24
