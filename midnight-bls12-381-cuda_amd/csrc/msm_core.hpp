@@ -553,6 +553,25 @@ MBLS_DEV RJac<F> row_tree(RJac<F> acc, uint8_t* sh, uint32_t r) {
     return acc;
 }
 
+// sum of n <= 16 Jacobian points ld(k) by the workgroup's 4 waves in the wave layout (a wave
+// addition spreads its independent products over the 4 rows: ~1/3 of a row addition's latency):
+// wave w adds points w, w + 4, ... (<= 3 additions), wave 0 adds the 3 other wave sums through
+// sh slots 1..3 (a wave writes only its own slot, read by no other wave before the barrier).
+// Result valid in wave 0.  6 dependent additions against the row tree's 4 x ~3.
+template <class F, class Ld>
+MBLS_DEV RJac<F> wave_sum16(uint8_t* sh, uint32_t n, Ld&& ld) {
+    using W = RedIO<F, MODE_WAVE>;
+    const uint32_t wv = threadIdx.x >> 6;
+    RJac<F> acc = wv < n ? ld(wv) : RJac<F>::inf();
+    for (uint32_t k = wv + 4; k < n; k += 4) acc = W::add(acc, ld(k));
+    W::st(sh, wv, acc);
+    __syncthreads();
+    if (wv == 0)
+        for (uint32_t k = 1; k < 4 && k < n; ++k) acc = W::add(acc, W::ld(sh, k));
+    __syncthreads();  // sh is reused by the caller
+    return acc;
+}
+
 // sum of the CHAINS Jacobian points in sh (lane layout), by rows; result in row 0
 template <class F>
 MBLS_DEV RJac<F> rows_sum_chains(uint8_t* sh, uint32_t chains) {
@@ -576,6 +595,24 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+MBLS_DEV bool load_j28(const uint8_t* __restrict__ base, size_t i, r28::F28& x, r28::F28& y, r28::F28& z) {
+    const uint4* q = reinterpret_cast<const uint4*>(base + i * 144);
+    uint32_t w[3][12], zany = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint4 u = q[3 * c + j];
+            w[c][4 * j] = u.x, w[c][4 * j + 1] = u.y, w[c][4 * j + 2] = u.z, w[c][4 * j + 3] = u.w;
+        }
+#pragma unroll
+    for (int j = 0; j < 12; ++j) zany |= w[2][j];
+    if (!zany) return false;  // the identity
+    x = r28::unpack_shift8(w[0]);
+    y = r28::unpack_shift8(w[1]);
+    z = r28::unpack_shift8(w[2]);
+    return true;
+}
 // r28 lane addition of chunk partial k (G1: the light path's and the slice chains' form)
 MBLS_DEV void r28_add_partial(r28::J28& acc, const uint8_t* __restrict__ partials, uint32_t k) {
     const uint4* q = reinterpret_cast<const uint4*>(partials + (size_t)k * 144);
@@ -684,21 +721,44 @@ MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t
         const uint32_t b = H.bucket[e];
         const uint32_t c0 = chunk_off[b] + (g - f0) * S;
         const uint32_t c1 = min(c0 + S, chunk_off[b + 1]);
+        // chains, then a lane tree down to 16 chain sums (log depth: a lane addition is ~1.3x a
+        // row addition's latency, but 16 rows summing 256 chains took 15 of them in series), then
+        // the rows
+        uint32_t live = min(CHAINS, c1 - c0);
         if constexpr (std::is_same<L, Fq>::value && MBLS_BS_R28) {
             r28::J28 acc = r28::J28::inf();
             for (uint32_t k = c0 + j; k < c1; k += CHAINS) r28_add_partial(acc, partials, k);
             store_jac28(sh, j, acc);
+            __syncthreads();
+            for (; live > 16; live = (live + 1) / 2) {
+                const uint32_t h = (live + 1) / 2;  // chain j < live - h takes chain j + h
+                if (j < live - h) {
+                    r28::F28 x, y, z;
+                    if (load_j28(sh, j + h, x, y, z)) r28::jadd(acc, x, y, z);
+                }
+                __syncthreads();
+                if (j < live - h) store_jac28(sh, j, acc);
+                __syncthreads();
+            }
         } else {
             Jacobian<L> acc = Jacobian<L>::inf();
             for (uint32_t k = c0 + j; k < c1; k += CHAINS) acc = jac_add(acc, load_jac<L>(partials, k));
             store_jac<L>(sh, j, acc);
+            __syncthreads();
+            for (; live > 16; live = (live + 1) / 2) {
+                const uint32_t h = (live + 1) / 2;
+                if (j < live - h) acc = jac_add(acc, load_jac<L>(sh, j + h));
+                __syncthreads();
+                if (j < live - h) store_jac<L>(sh, j, acc);
+                __syncthreads();
+            }
         }
-        __syncthreads();
-        const RJac<F> ssum = rows_sum_chains<F>(sh, min(CHAINS, c1 - c0));
+        using WIO = RedIO<F, MODE_WAVE>;
+        const RJac<F> ssum = wave_sum16<F>(sh, live, [&](uint32_t k) { return WIO::ld(sh, k); });
 #if MBLS_HEAVY_TRACE
         trs = wall_clock64();
 #endif
-        if (threadIdx.x < 16) IO::st(H.res, g, ssum);
+        if (threadIdx.x < 64) WIO::st(H.res, g, ssum);
         __threadfence();
         __syncthreads();
         const uint32_t r = threadIdx.x >> 4;
@@ -712,9 +772,8 @@ MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t
             __syncthreads();
             if (!last) continue;  // workgroup-uniform; sh and `last` are rewritten after barriers
             __threadfence();
-            RJac<F> gsum = r < gs ? IO::ld(H.res, gl + r) : RJac<F>::inf();
-            gsum = row_tree<F>(gsum, sh, r);
-            if (threadIdx.x < 16) IO::st(H.res, gl, gsum);
+            const RJac<F> gsum = wave_sum16<F>(sh, gs, [&](uint32_t k) { return WIO::ld(H.res, gl + k); });
+            if (threadIdx.x < 64) WIO::st(H.res, gl, gsum);
 #if MBLS_HEAVY_TRACE
             trg = wall_clock64();
 #endif
@@ -732,10 +791,15 @@ MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t
 #if MBLS_HEAVY_TRACE
             const uint64_t trf1 = wall_clock64();
 #endif
-            RJac<F> tot = r < nsum ? IO::ld(H.res, f0 + r * step) : RJac<F>::inf();
-            for (uint32_t k = r + 16; k < nsum; k += 16) tot = IO::add(tot, IO::ld(H.res, f0 + k * step));
-            tot = row_tree<F>(tot, sh, r);
-            if (threadIdx.x < 16) IO::st(buckets, b, tot);
+            if (nsum <= 16) {  // workgroup-uniform
+                const RJac<F> tot = wave_sum16<F>(sh, nsum, [&](uint32_t k) { return WIO::ld(H.res, f0 + k * step); });
+                if (threadIdx.x < 64) WIO::st(buckets, b, tot);
+            } else {
+                RJac<F> tot = r < nsum ? IO::ld(H.res, f0 + r * step) : RJac<F>::inf();
+                for (uint32_t k = r + 16; k < nsum; k += 16) tot = IO::add(tot, IO::ld(H.res, f0 + k * step));
+                tot = row_tree<F>(tot, sh, r);
+                if (threadIdx.x < 16) IO::st(buckets, b, tot);
+            }
 #if MBLS_HEAVY_TRACE
             const uint64_t trb = wall_clock64();
             if (threadIdx.x == 0)
@@ -853,24 +917,6 @@ __global__ __launch_bounds__(256) void k_reduce_scaled(const uint8_t* __restrict
 #ifndef MBLS_RED_R28
 #define MBLS_RED_R28 1
 #endif
-MBLS_DEV bool load_j28(const uint8_t* __restrict__ base, size_t i, r28::F28& x, r28::F28& y, r28::F28& z) {
-    const uint4* q = reinterpret_cast<const uint4*>(base + i * 144);
-    uint32_t w[3][12], zany = 0;
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const uint4 u = q[3 * c + j];
-            w[c][4 * j] = u.x, w[c][4 * j + 1] = u.y, w[c][4 * j + 2] = u.z, w[c][4 * j + 3] = u.w;
-        }
-#pragma unroll
-    for (int j = 0; j < 12; ++j) zany |= w[2][j];
-    if (!zany) return false;  // the identity
-    x = r28::unpack_shift8(w[0]);
-    y = r28::unpack_shift8(w[1]);
-    z = r28::unpack_shift8(w[2]);
-    return true;
-}
 template <class F>  // F = Fq only
 __global__ __launch_bounds__(256) void k_reduce_scaled_r28(const uint8_t* __restrict__ V, const uint8_t* __restrict__ U,
                                                            uint32_t m_in, uint32_t seg_log, int Wg, int off,
