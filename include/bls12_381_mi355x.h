@@ -318,15 +318,21 @@ void mbls_profile_enable(int on);
 void mbls_profile_reset(void);
 int mbls_profile_read(const char** names, double* total_ms, long* counts, int max);
 
-/* Scheduling extension (no reference counterpart): the NEXT MSM enqueued on `stream` (a single
- * MSM, batch_size 1, on this device) records `event` on that stream once its bucket accumulation
- * has been enqueued, i.e. the event completes when the MSM enters its latency-bound tail (bucket
- * sums, reduction levels, final fold: ~2.5 ms of few-wave chains for G2 2^20).  Work made to wait
- * on it from another stream -- a batch of NTTs, say -- then fills the SIMDs the tail leaves idle
- * instead of time-slicing them with the VALU-bound accumulation (config #5, bench.py mix leg;
- * give the MSM's stream the higher priority).  One pending event per stream; a later call
- * replaces it; mbls_msm_accumulate_event(stream, NULL) clears it.  The event is the caller's. */
+/* Scheduling extension (no reference counterpart): the NEXT MSM call on `stream` takes `event`
+ * and records it on that stream once its (last member's) bucket accumulation has been enqueued,
+ * i.e. the event completes when the MSM enters its latency-bound tail (bucket sums, reduction
+ * levels, final fold: ~2.5 ms of few-wave chains for G2 2^20).  Work made to wait on it from
+ * another stream -- a batch of NTTs, say -- then fills the SIMDs the tail leaves idle instead of
+ * time-slicing them with the VALU-bound accumulation (config #5, bench.py mix leg; give the MSM's
+ * stream the higher priority).  Every MSM call that gets past its argument checks takes the
+ * pending event: a batch records it after the LAST member's accumulation; an empty MSM, a
+ * multi-device call (at its end, on the caller's stream) and a call that fails after taking it
+ * record it where they stop, so it never lingers for an unrelated later MSM.  One pending event
+ * per stream; a later call replaces it; mbls_msm_accumulate_event(stream, NULL) clears it.  The
+ * event is the caller's: mbls_msm_accumulate_event_drop(event) removes every pending
+ * registration of it (call it before destroying an event that may still be pending). */
 eIcicleError mbls_msm_accumulate_event(void* stream, void* event);
+eIcicleError mbls_msm_accumulate_event_drop(void* event);
 
 #ifdef __cplusplus
 }

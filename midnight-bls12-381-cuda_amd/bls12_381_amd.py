@@ -77,7 +77,7 @@ EXPORTED = [
     "mbls_release_stream", "mbls_release_scratch", "mbls_scratch_stats",
     "mbls_g1_msm_multi_device", "mbls_g2_msm_multi_device", "bls12_381_vector_sum",
     "bls12_381_g1_affine_to_projective", "bls12_381_g1_projective_to_affine", "bls12_381_g2_projective_to_affine",
-    "mbls_msm_plan", "mbls_msm_accumulate_event",
+    "mbls_msm_plan", "mbls_msm_accumulate_event", "mbls_msm_accumulate_event_drop",
 ]
 
 _LIB = None
@@ -121,7 +121,7 @@ def lib():
         "bls12_381_g1_affine_to_projective": [P, i32, P, P], "bls12_381_g1_projective_to_affine": [P, i32, P, P],
         "bls12_381_g2_projective_to_affine": [P, i32, P, P],
         "mbls_msm_plan": [i32, i32, P, P],
-        "mbls_msm_accumulate_event": [P, P],
+        "mbls_msm_accumulate_event": [P, P], "mbls_msm_accumulate_event_drop": [P],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -426,8 +426,18 @@ class HipEvent:
         if self.hip.hipStreamWaitEvent(_stream_handle(stream), self.ev, 0) != 0:
             raise RuntimeError("hipStreamWaitEvent failed")
 
+    def query(self):
+        """True when the event has completed (or was never recorded), False while pending"""
+        self.hip.hipEventQuery.argtypes = [ctypes.c_void_p]
+        r = self.hip.hipEventQuery(self.ev)
+        if r not in (0, 600):  # hipSuccess, hipErrorNotReady
+            raise RuntimeError(f"hipEventQuery failed ({r})")
+        return r == 0
+
     def __del__(self):
         try:
+            # a registration still pending for this event must not outlive it (ADVICE r5)
+            lib().mbls_msm_accumulate_event_drop(self.ev)
             self.hip.hipEventDestroy(self.ev)
         except Exception:
             pass

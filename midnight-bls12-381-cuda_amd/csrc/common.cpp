@@ -362,6 +362,20 @@ eIcicleError mbls_msm_accumulate_event(void* stream, void* event) {
     return MBLS_SUCCESS;
 }
 
+eIcicleError mbls_msm_accumulate_event_drop(void* event) {
+    if (!event) return MBLS_SUCCESS;
+    std::lock_guard<std::mutex> g(mbls::g_acc_ev_mu);
+    for (auto it = mbls::g_acc_ev->begin(); it != mbls::g_acc_ev->end();) {
+        if (it->second == static_cast<hipEvent_t>(event)) {
+            it = mbls::g_acc_ev->erase(it);
+            mbls::g_acc_ev_n.fetch_sub(1, std::memory_order_relaxed);
+        } else {
+            ++it;
+        }
+    }
+    return MBLS_SUCCESS;
+}
+
 eIcicleError mbls_release_stream(void* stream) {
     mbls::Pool& P = mbls::pool();
     std::lock_guard<std::mutex> g(P.mu);

@@ -118,6 +118,24 @@ const void* pinned_host_device_pointer(const void* p);
 size_t device_bytes_from(const void* p);
 // the event mbls_msm_accumulate_event left pending for `st` (taken: nullptr afterwards), or nullptr
 hipEvent_t take_accumulate_event(hipStream_t st);
+// a taken accumulate event: recorded on `st` when the guard dies unless release()d first (the
+// MSM paths that never reach an accumulation -- empty MSMs, errors -- still record it, so it
+// cannot linger for an unrelated later MSM: ADVICE r5)
+struct AccEventGuard {
+    hipEvent_t ev;
+    hipStream_t st;
+    AccEventGuard(hipEvent_t e, hipStream_t s) : ev(e), st(s) {}
+    AccEventGuard(const AccEventGuard&) = delete;
+    AccEventGuard& operator=(const AccEventGuard&) = delete;
+    hipEvent_t release() {
+        hipEvent_t e = ev;
+        ev = nullptr;
+        return e;
+    }
+    ~AccEventGuard() {
+        if (ev) (void)hipEventRecord(ev, st);
+    }
+};
 
 // Stage profiler: when enabled (mbls_profile_enable / MBLS_PROFILE=1) a ProfScope records a
 // hipEvent pair on the stream around the enclosed launches; mbls_profile_read() sums the

@@ -1430,10 +1430,14 @@ struct TailPipe {
 template <class F>
 eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t* bases, uint32_t n,
                         const MsmPlan& P, uint8_t* result, StreamCtx& ctx, hipStream_t st,
-                        uint8_t* icicle_out = nullptr, const TailPipe* pipe = nullptr) {
+                        uint8_t* icicle_out = nullptr, const TailPipe* pipe = nullptr,
+                        hipEvent_t acc_event = nullptr) {
     Arena& arena = ctx.arena;
     constexpr size_t JAC = GroupTraits<F>::JAC, AFF = GroupTraits<F>::AFF;
     constexpr uint32_t LN = LaneOf<F>::LANES;  // lanes per chain in the lane-mode kernels
+    // mbls_msm_accumulate_event: recorded after the accumulation launch below, or wherever this
+    // function returns before it (an empty MSM, an error)
+    AccEventGuard acc_ev(acc_event, st);
     if (n == 0) {
         hipLaunchKernelGGL(k_store_inf<F>, dim3(1), dim3(64), 0, st, result, 1);
         if (icicle_out) hipLaunchKernelGGL(k_jac_to_icicle<F>, dim3(1), dim3(64), 0, st, result, icicle_out, 1);
@@ -1575,9 +1579,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         hipLaunchKernelGGL(accumulate_kernel<F>(), dim3((threads + 255) / 256), dim3(256), 0, st, sorted, offsets,
                            chunk_off, first, 0u, TB, acc_b, acc_phi, nsplit, P.chunk, partials);
     }
-    if (!pipe) {  // mbls_msm_accumulate_event: the tail starts here (single MSMs only)
-        if (hipEvent_t ev = take_accumulate_event(st)) MBLS_TRY(hipEventRecord(ev, st));
-    }
+    // mbls_msm_accumulate_event: the tail starts here (the caller passes it to the last member)
+    if (hipEvent_t e = acc_ev.release()) MBLS_TRY(hipEventRecord(e, st));
     {
         ProfScope ps("msm.bucket_sum", st);
         // light buckets one thread each, heavy buckets by slice workgroups in the same launch
@@ -1644,9 +1647,12 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     const bool icicle_semantics = entry != MSM_RAW;
     constexpr size_t AFF = GroupTraits<F>::AFF, JAC = GroupTraits<F>::JAC;
     if (!cfg || !results) return MBLS_INVALID_POINTER;
+    hipStream_t st = static_cast<hipStream_t>(cfg->stream);
+    // a pending mbls_msm_accumulate_event belongs to this call whatever happens below: the last
+    // member's accumulation records it (msm_device), any earlier return records it here
+    AccEventGuard acc_ev(take_accumulate_event(st), st);
     if (msm_size < 0 || msm_size > (1 << MAX_MSM_LOG)) return MBLS_INVALID_ARGUMENT;
     if (msm_size > 0 && (!scalars || !bases)) return MBLS_INVALID_POINTER;
-    hipStream_t st = static_cast<hipStream_t>(cfg->stream);
     const int batch = icicle_semantics ? (cfg->batch_size > 0 ? cfg->batch_size : 1) : 1;
     // The reference's plain device-bases MSMs (core/msm.rs:897-913, 1025-1040, 1097-1110) set
     // cfg.precompute_factor = MIDNIGHT_GPU_PRECOMPUTE on a buffer of n plain bases; its backend
@@ -1760,7 +1766,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
         // piped ICICLE members are normalised inside their tails (hidden but for the last one)
         uint8_t* icicle_b = direct ? direct : (piped && entry == MSM_ICICLE ? d_r + (size_t)b * JAC : nullptr);
         er = msm_device<F>(sb, scal_mont, bb, (uint32_t)n, P, d_r + (size_t)b * JAC, ctx, st, icicle_b,
-                           piped ? &pipe : nullptr);
+                           piped ? &pipe : nullptr, b == batch - 1 ? acc_ev.release() : nullptr);
         if (er != MBLS_SUCCESS) return er;
         if (piped) MBLS_TRY(hipEventRecord(ctx.events[4 + (b & 1)], pipe.side));
     }
@@ -1840,6 +1846,9 @@ eIcicleError msm_multi_device(const void* scalars, const void* const* bases_per_
     // shard streams are forked from the caller's stream: the caller's earlier work on its
     // inputs (a device scalar upload, say) is ordered before every shard
     MBLS_TRY(hipSetDevice(d0));
+    // a pending mbls_msm_accumulate_event of the caller's stream: taken here (so the first shard's
+    // msm_call on st0 does not), recorded on st0 when this call returns
+    AccEventGuard acc_ev(take_accumulate_event(st0), st0);
     // the previous call may still read or write the partial / gather slots on its own streams
     // (is_async with a caller stream): this call's fork -- and so every shard -- waits for its end
     if (MultiDevRes* last = multi_device_last()) MBLS_TRY(hipStreamWaitEvent(st0, last->done, 0));

@@ -279,3 +279,59 @@ def test_msm_accumulate_event_orders_a_second_stream(amd, gh):
     amd.msm_accumulate_event(s_a, None)  # cleared: the next MSM records nothing
     r = amd.msm("g2", s, b, scalars_mont=True, stream=s_a, n=n)
     assert gh.decode_icicle("g2", r[0]) == ref
+
+
+def test_msm_accumulate_event_taken_by_every_msm(amd, gh):
+    """the pending event is taken by the next MSM call on the stream whatever its
+    shape -- an empty MSM records it where it stops, a batch after its LAST member's accumulation --
+    and a later single MSM finds nothing pending.  Observed with hipEventQuery right after the
+    enqueue, behind a ~2 ms NTT batch on the same stream: a recorded event is still pending then,
+    an unrecorded (or already completed) one reads complete."""
+    import torch
+    n, nn, nb = 1 << 12, 1 << 22, 4
+    s = torch.zeros((2 * n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0B51, montgomery=True)
+    b = torch.zeros((n, 12), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g1", b, 0x5EED0B52)
+    x = torch.zeros((nb * nn, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(x, 0x5EED0B53, montgomery=True)
+    y = torch.zeros_like(x)
+    amd.ntt_init_domain()
+    torch.cuda.synchronize()
+    s_a = torch.cuda.Stream()
+
+    def busy():  # a few ms of NTT work queued ahead on s_a
+        amd.ntt(x, out=y, stream=s_a, is_async=True, batch=nb)
+
+    single = amd.msm("g1", s[:n], b, scalars_mont=True, n=n)
+    out = torch.zeros((2, 18), dtype=torch.int64, device="cuda")
+
+    def call(shape):
+        if shape == "empty":
+            amd.msm("g1", s[:0], b[:0], scalars_mont=True, out=out[:1], stream=s_a, is_async=True, n=0)
+        else:
+            amd.msm("g1", s, b, scalars_mont=True, out=out, stream=s_a, is_async=True, n=n, batch=2)
+
+    for shape in ("empty", "batch"):  # warm the stream's scratch: no allocation (and its sync) below
+        busy()
+        call(shape)
+    torch.cuda.synchronize()
+    for shape in ("empty", "batch"):
+        ev = amd.HipEvent()
+        torch.cuda.synchronize()
+        amd.msm_accumulate_event(s_a, ev.handle)
+        busy()
+        call(shape)
+        assert not ev.query(), f"{shape}: the MSM did not record the pending event"
+        torch.cuda.synchronize()
+        assert ev.query()
+        if shape == "batch":
+            assert np.array_equal(amd.to_numpy_u64(out)[0], single[0])
+        # nothing pending now: a single MSM behind busy work does not record the event again
+        busy()
+        r = amd.msm("g1", s[:n], b, scalars_mont=True, out=torch.zeros((1, 18), dtype=torch.int64, device="cuda"),
+                    stream=s_a, is_async=True, n=n)
+        assert ev.query(), f"{shape}: the event stayed pending for a later MSM"
+        torch.cuda.synchronize()
+        assert np.array_equal(amd.to_numpy_u64(r), single)
+        del ev  # __del__ drops any registration before destroying the event
