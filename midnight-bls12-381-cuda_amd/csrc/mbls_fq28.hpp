@@ -26,6 +26,7 @@
 //   * `fold` carries and subtracts q p with q from the top limb: normalised, < 3p.
 #pragma once
 #include "mbls_field.hpp"
+#include "mbls_madchain.hpp"
 
 namespace mbls {
 namespace r28 {
@@ -67,26 +68,58 @@ struct F28 {
 
 // ------------------------------------------------------------------------- products
 // Montgomery product (a b + m p) / 2^392, product scanning; column k accumulates its
-// a_i b_(k-i) and m_i p_(k-i) in ONE 64-bit register, v_mad_u64_u32 each.
+// a_i b_(k-i) and m_i p_(k-i) in ONE 64-bit register as one v_mad_u64_u32 chain (mbls_madchain.hpp:
+// written as C++ additions LLVM gave every column a fresh chain plus a 64-bit merge add, ~39
+// extra instructions per product).  Columns by compile-time recursion; SQ: the square's column
+// (cross products against the doubled operand d, then the diagonal term); C2/D2: mul2's second
+// product.
+template <int K>
+MBLS_DEV void reduce_col(uint64_t& acc, uint32_t (&m)[NL], F28& r) {
+    constexpr int LO = K > NL - 1 ? K - (NL - 1) : 0;
+    madc::col<K, LO, (K < NL ? K : NL) - 1, true>(acc, m, P);
+    if constexpr (K < NL) {
+        m[K] = ((uint32_t)acc * NINV) & MASK;
+        madc::mad1<true>(acc, m[K], P[0]);  // the low 28 bits become zero
+    } else {
+        r.l[K - NL] = (uint32_t)acc & MASK;
+    }
+    acc >>= 28;
+}
+template <int K>
+MBLS_DEV void mul_cols(uint64_t& acc, uint32_t (&m)[NL], F28& r, const F28& a, const F28& b) {
+    if constexpr (K < 2 * NL - 1) {
+        madc::col<K, (K > NL - 1 ? K - (NL - 1) : 0), (K < NL - 1 ? K : NL - 1), false>(acc, a.l, b.l);
+        reduce_col<K>(acc, m, r);
+        mul_cols<K + 1>(acc, m, r, a, b);
+    }
+}
+template <int K>
+MBLS_DEV void mul2_cols(uint64_t& acc, uint32_t (&m)[NL], F28& r, const F28& a, const F28& b, const F28& c,
+                        const F28& d) {
+    if constexpr (K < 2 * NL - 1) {
+        constexpr int LO = K > NL - 1 ? K - (NL - 1) : 0, HI = K < NL - 1 ? K : NL - 1;
+        madc::col<K, LO, HI, false>(acc, a.l, b.l);
+        madc::col<K, LO, HI, false>(acc, c.l, d.l);
+        reduce_col<K>(acc, m, r);
+        mul2_cols<K + 1>(acc, m, r, a, b, c, d);
+    }
+}
+template <int K>
+MBLS_DEV void sqr_cols(uint64_t& acc, uint32_t (&m)[NL], F28& r, const F28& a, const uint32_t (&d)[NL]) {
+    if constexpr (K < 2 * NL - 1) {
+        constexpr int LO = K > NL - 1 ? K - (NL - 1) : 0;
+        madc::col<K, LO, (K + 1) / 2 - 1, false>(acc, a.l, d);  // i < k - i: a_i (2 a_(k-i)) (none at k = 0)
+        if constexpr ((K & 1) == 0) madc::mad1<false>(acc, a.l[K >> 1], a.l[K >> 1]);
+        reduce_col<K>(acc, m, r);
+        sqr_cols<K + 1>(acc, m, r, a, d);
+    }
+}
+
 MBLS_DEV F28 mul(const F28& a, const F28& b) {
     uint32_t m[NL];
     F28 r;
     uint64_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < 2 * NL - 1; ++k) {
-#pragma unroll
-        for (int i = (k > NL - 1 ? k - (NL - 1) : 0); i <= (k < NL - 1 ? k : NL - 1); ++i)
-            acc += (uint64_t)a.l[i] * b.l[k - i];
-#pragma unroll
-        for (int i = (k > NL - 1 ? k - (NL - 1) : 0); i < (k < NL ? k : NL); ++i) acc += (uint64_t)m[i] * P[k - i];
-        if (k < NL) {
-            m[k] = ((uint32_t)acc * NINV) & MASK;
-            acc += (uint64_t)m[k] * P[0];
-        } else {
-            r.l[k - NL] = (uint32_t)acc & MASK;
-        }
-        acc >>= 28;
-    }
+    mul_cols<0>(acc, m, r, a, b);
     r.l[NL - 1] = (uint32_t)acc;
     return r;
 }
@@ -96,23 +129,7 @@ MBLS_DEV F28 mul2(const F28& a, const F28& b, const F28& c, const F28& d) {
     uint32_t m[NL];
     F28 r;
     uint64_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < 2 * NL - 1; ++k) {
-#pragma unroll
-        for (int i = (k > NL - 1 ? k - (NL - 1) : 0); i <= (k < NL - 1 ? k : NL - 1); ++i) {
-            acc += (uint64_t)a.l[i] * b.l[k - i];
-            acc += (uint64_t)c.l[i] * d.l[k - i];
-        }
-#pragma unroll
-        for (int i = (k > NL - 1 ? k - (NL - 1) : 0); i < (k < NL ? k : NL); ++i) acc += (uint64_t)m[i] * P[k - i];
-        if (k < NL) {
-            m[k] = ((uint32_t)acc * NINV) & MASK;
-            acc += (uint64_t)m[k] * P[0];
-        } else {
-            r.l[k - NL] = (uint32_t)acc & MASK;
-        }
-        acc >>= 28;
-    }
+    mul2_cols<0>(acc, m, r, a, b, c, d);
     r.l[NL - 1] = (uint32_t)acc;
     return r;
 }
@@ -124,22 +141,7 @@ MBLS_DEV F28 sqr(const F28& a) {
     for (int i = 0; i < NL; ++i) d[i] = a.l[i] << 1;
     F28 r;
     uint64_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < 2 * NL - 1; ++k) {
-        const int lo = k > NL - 1 ? k - (NL - 1) : 0;
-#pragma unroll
-        for (int i = lo; 2 * i < k; ++i) acc += (uint64_t)a.l[i] * d[k - i];
-        if ((k & 1) == 0) acc += (uint64_t)a.l[k >> 1] * a.l[k >> 1];
-#pragma unroll
-        for (int i = lo; i < (k < NL ? k : NL); ++i) acc += (uint64_t)m[i] * P[k - i];
-        if (k < NL) {
-            m[k] = ((uint32_t)acc * NINV) & MASK;
-            acc += (uint64_t)m[k] * P[0];
-        } else {
-            r.l[k - NL] = (uint32_t)acc & MASK;
-        }
-        acc >>= 28;
-    }
+    sqr_cols<0>(acc, m, r, a, d);
     r.l[NL - 1] = (uint32_t)acc;
     return r;
 }

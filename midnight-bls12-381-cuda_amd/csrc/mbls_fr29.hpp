@@ -26,6 +26,7 @@
 //     < 1.04 r -- in [0, 2r) and below 2^256, so the lazy butterflies take it as words.
 #pragma once
 #include "mbls_field.hpp"
+#include "mbls_madchain.hpp"
 
 namespace mbls {
 namespace r29 {
@@ -71,26 +72,30 @@ MBLS_DEV Fr pack(const F29& a) {
 }
 
 // Montgomery product a b / 2^261 (lazy: no final subtraction), product scanning; column k
-// accumulates its a_i b_(k-i) and m_i r_(k-i) in ONE 64-bit register, v_mad_u64_u32 each.
+// accumulates its a_i b_(k-i) and m_i r_(k-i) in ONE 64-bit register, one v_mad_u64_u32 chain
+// (mbls_madchain.hpp: written as C++ additions LLVM splits every column into a fresh chain plus a
+// 64-bit merge add).  Columns by compile-time recursion.
+template <int K>
+MBLS_DEV void mul_cols(uint64_t& acc, uint32_t (&m)[NL], F29& r, const F29& a, const F29& b) {
+    if constexpr (K < 2 * NL - 1) {
+        constexpr int LO = K > NL - 1 ? K - (NL - 1) : 0;
+        madc::col<K, LO, (K < NL - 1 ? K : NL - 1), false>(acc, a.l, b.l);
+        madc::col<K, LO, (K < NL ? K : NL) - 1, true>(acc, m, RL);
+        if constexpr (K < NL) {
+            m[K] = (0u - (uint32_t)acc) & MASK;
+            acc += m[K];  // m_k r_0, r_0 = 1: the low 29 bits become zero
+        } else {
+            r.l[K - NL] = (uint32_t)acc & MASK;
+        }
+        acc >>= 29;
+        mul_cols<K + 1>(acc, m, r, a, b);
+    }
+}
 MBLS_DEV F29 mul(const F29& a, const F29& b) {
     uint32_t m[NL];
     F29 r;
     uint64_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < 2 * NL - 1; ++k) {
-#pragma unroll
-        for (int i = (k > NL - 1 ? k - (NL - 1) : 0); i <= (k < NL - 1 ? k : NL - 1); ++i)
-            acc += (uint64_t)a.l[i] * b.l[k - i];
-#pragma unroll
-        for (int i = (k > NL - 1 ? k - (NL - 1) : 0); i < (k < NL ? k : NL); ++i) acc += (uint64_t)m[i] * RL[k - i];
-        if (k < NL) {
-            m[k] = (0u - (uint32_t)acc) & MASK;
-            acc += m[k];  // m_k r_0, r_0 = 1: the low 29 bits become zero
-        } else {
-            r.l[k - NL] = (uint32_t)acc & MASK;
-        }
-        acc >>= 29;
-    }
+    mul_cols<0>(acc, m, r, a, b);
     r.l[NL - 1] = (uint32_t)acc;
     return r;
 }

@@ -1,0 +1,288 @@
+"""Limb-exact Python model of csrc/mbls_fq28.hpp and csrc/mbls_fr29.hpp (test infrastructure).
+
+Each function follows its header's algorithm step for step on raw limbs -- the same column order,
+the same 64-bit accumulator, the same masks and shifts -- and ASSERTS the hardware limits the
+header's bound table relies on: every column accumulator stays below 2^64 (v_mad_u64_u32 has no
+carry-out into the next column), every uint32 limb stays below 2^32, fold's int64 stays in range.
+tests/test_gpu_limbs.py runs its extreme-limb cases through this model on the CPU (the bounds as
+an executable proof) and through the GPU probe (the device code itself), and checks both against
+Python integers."""
+
+U64 = 1 << 64
+U32 = 1 << 32
+
+
+class Overflow(AssertionError):
+    pass
+
+
+def _chk64(acc, what):
+    if not 0 <= acc < U64:
+        raise Overflow(f"{what}: column accumulator {acc:#x} >= 2^64")
+    return acc
+
+
+def _chk32(v, what):
+    if not 0 <= v < U32:
+        raise Overflow(f"{what}: limb {v:#x} outside uint32")
+    return v
+
+
+# ------------------------------------------------------------------ radix 2^28 Fq (mbls_fq28.hpp)
+class Fq28:
+    NL, MASK = 14, (1 << 28) - 1
+
+    def __init__(self, P, ninv, fold_recip):
+        self.P = [(P >> (28 * i)) & self.MASK for i in range(13)] + [P >> (28 * 13)]
+        self.NINV, self.FOLD_RECIP = ninv, fold_recip
+
+    def _reduce_col(self, acc, m, r, k, what):
+        NL = self.NL
+        lo = k - (NL - 1) if k > NL - 1 else 0
+        for i in range(lo, min(k, NL)):
+            acc = _chk64(acc + m[i] * self.P[k - i], what)
+        if k < NL:
+            m[k] = ((acc & 0xffffffff) * self.NINV) & self.MASK
+            acc = _chk64(acc + m[k] * self.P[0], what)
+        else:
+            r[k - NL] = acc & self.MASK
+        return acc >> 28
+
+    def mul(self, a, b):
+        return self.mul2(a, b, None, None)
+
+    def mul2(self, a, b, c, d):
+        NL = self.NL
+        for x in (a, b) + ((c, d) if c is not None else ()):
+            for v in x:
+                _chk32(v, "operand")
+        m, r, acc = [0] * NL, [0] * NL, 0
+        for k in range(2 * NL - 1):
+            lo, hi = (k - (NL - 1) if k > NL - 1 else 0), (k if k < NL - 1 else NL - 1)
+            for i in range(lo, hi + 1):
+                acc = _chk64(acc + a[i] * b[k - i], "mul")
+            if c is not None:
+                for i in range(lo, hi + 1):
+                    acc = _chk64(acc + c[i] * d[k - i], "mul2")
+            acc = self._reduce_col(acc, m, r, k, "mul reduction")
+        r[NL - 1] = _chk32(acc, "mul top limb")
+        return r
+
+    def sqr(self, a):
+        NL = self.NL
+        d = [_chk32(v << 1, "sqr doubled operand") for v in a]
+        m, r, acc = [0] * NL, [0] * NL, 0
+        for k in range(2 * NL - 1):
+            lo = k - (NL - 1) if k > NL - 1 else 0
+            i = lo
+            while 2 * i < k:
+                acc = _chk64(acc + a[i] * d[k - i], "sqr")
+                i += 1
+            if k % 2 == 0:
+                acc = _chk64(acc + a[k >> 1] * a[k >> 1], "sqr diagonal")
+            acc = self._reduce_col(acc, m, r, k, "sqr reduction")
+        r[NL - 1] = _chk32(acc, "sqr top limb")
+        return r
+
+    def add(self, a, b):
+        return [_chk32(x + y, "add") for x, y in zip(a, b)]
+
+    def sub(self, bk, a, b):
+        return [_chk32(x + (k - y), "sub") for x, y, k in zip(a, b, bk)]
+
+    def neg(self, bk, b):
+        return [_chk32(k - y, "neg") for y, k in zip(b, bk)]
+
+    def x2(self, a):
+        return [_chk32(v << 1, "x2") for v in a]
+
+    def x4(self, a):
+        return [_chk32(v << 2, "x4") for v in a]
+
+    def carry(self, a):
+        r, c = [0] * self.NL, 0
+        for i in range(self.NL - 1):
+            t = _chk32(a[i] + c, "carry")
+            r[i], c = t & self.MASK, t >> 28
+        r[-1] = _chk32(a[-1] + c, "carry top")
+        return r
+
+    def fold(self, a):
+        for v in a:
+            _chk32(v, "fold input")
+        top = (a[-1] + (a[-2] >> 28)) % U32
+        nq = -(((top * self.FOLD_RECIP) % U64) >> 40)
+        r, c = [0] * self.NL, 0
+        for i in range(self.NL):
+            t = nq * self.P[i] + c + a[i]
+            if not -(1 << 63) <= t < (1 << 63):
+                raise Overflow("fold int64")
+            r[i], c = t & self.MASK, t >> 28
+        r[-1] = (r[-1] + ((c << 28) % U32)) % U32
+        return r
+
+
+# ------------------------------------------------------------------ radix 2^29 Fr (mbls_fr29.hpp)
+class Fr29:
+    NL, MASK = 9, (1 << 29) - 1
+
+    def __init__(self, R):
+        self.RL = [(R >> (29 * i)) & self.MASK for i in range(8)] + [R >> (29 * 8)]
+
+    def mul(self, a, b):
+        NL = self.NL
+        for x in (a, b):
+            for v in x:
+                _chk32(v, "operand")
+        m, r, acc = [0] * NL, [0] * NL, 0
+        for k in range(2 * NL - 1):
+            lo, hi = (k - (NL - 1) if k > NL - 1 else 0), (k if k < NL - 1 else NL - 1)
+            for i in range(lo, hi + 1):
+                acc = _chk64(acc + a[i] * b[k - i], "fr mul")
+            for i in range(lo, min(k, NL)):
+                acc = _chk64(acc + m[i] * self.RL[k - i], "fr reduction")
+            if k < NL:
+                m[k] = (-(acc & 0xffffffff)) % U32 & self.MASK
+                acc = _chk64(acc + m[k], "fr reduction")
+            else:
+                r[k - NL] = acc & self.MASK
+            acc >>= 29
+        r[NL - 1] = _chk32(acc, "fr top limb")
+        return r
+
+
+# ------------------------------------------------------------------ the accumulation's formulas
+def _fq28_formulas(F, B16, B32, B512, ONE):
+    """r28::is_zero_lt2p / is_zero_mod / dbl / madd / mmadd / to_words over the model F"""
+    P = F.P
+
+    def is_zero_lt2p(a):
+        return all(v == 0 for v in a) or all(v == p for v, p in zip(a, P))
+
+    def is_zero_mod(a):
+        v = F.fold(a)
+        p2, c = [], 0
+        for p in P:
+            t = (p << 1) + c
+            c = t >> 28
+            p2.append(t & F.MASK)
+        return all(x == 0 for x in v) or v == P or v == p2
+
+    def dbl(x, y, z):
+        A, B = F.sqr(x), F.sqr(y)
+        E = F.add(F.x2(A), A)
+        D = F.mul(F.x4(x), B)
+        C8 = F.mul(F.x4(F.x2(B)), B)
+        X3 = F.fold(F.sub(B32, F.sqr(E), F.x2(D)))
+        Y3 = F.fold(F.sub(B16, F.mul(E, F.sub(B16, D, X3)), C8))
+        return X3, Y3, F.mul(F.x2(y), z)
+
+    def madd(acc, x2_, y2_):
+        x, y, z = acc
+        if all(v == 0 for v in z):
+            return F.fold(x2_), F.fold(y2_), list(ONE)
+        Z1Z1 = F.sqr(z)
+        H = F.sub(B16, F.mul(x2_, Z1Z1), x)
+        Rr = F.sub(B16, F.mul(F.mul(y2_, z), Z1Z1), y)
+        HH = F.sqr(H)
+        if is_zero_lt2p(HH):
+            return dbl(x, y, z) if is_zero_mod(Rr) else (list(ONE), list(ONE), [0] * 14)
+        I = F.x4(HH)
+        J = F.mul(H, I)
+        Z3 = F.mul(F.x2(z), H)
+        V = F.mul(x, I)
+        R2 = F.carry(F.x2(Rr))
+        X3 = F.fold(F.sub(B32, F.sub(B16, F.sqr(R2), J), F.x2(V)))
+        Y3 = F.mul2(R2, F.sub(B16, V, X3), F.neg(B32, F.x2(y)), J)
+        return X3, Y3, Z3
+
+    def mmadd(acc, x2_, y2_):
+        x, y, _ = acc
+        H = F.fold(F.sub(B512, x2_, x))
+        HH = F.sqr(H)
+        if is_zero_lt2p(HH):
+            return None
+        I = F.x4(HH)
+        J = F.mul(H, I)
+        Z3 = F.x2(H)
+        V = F.mul(x, I)
+        R2 = F.x2(F.fold(F.sub(B512, y2_, y)))
+        X3 = F.fold(F.sub(B32, F.sub(B16, F.sqr(R2), J), F.x2(V)))
+        Y3 = F.mul2(R2, F.sub(B16, V, X3), F.neg(B32, F.x2(y)), J)
+        return X3, Y3, Z3
+
+    def to_words(a, Pint):
+        v = F.fold(a)
+        k = (v[0] * 0xfd) & 0xff
+        c, t = 0, []
+        for i in range(14):
+            c += v[i] + k * P[i]
+            t.append(c & F.MASK)
+            c >>= 28
+        if c:
+            raise Overflow("to_words: (v + k p) >= 2^392")
+        x = sum(x << (28 * i) for i, x in enumerate(t)) >> 8
+        for _ in range(2):
+            if x >= Pint:
+                x -= Pint
+        return [(x >> (32 * j)) & 0xffffffff for j in range(12)]
+
+    return is_zero_mod, madd, mmadd, to_words
+
+
+class Model:
+    """the GPU probe's interface (tests/diag/limbs_diag.hip op codes) over the limb model"""
+
+    def __init__(self, P, R, ninv, fold_recip, B16, B32, B512, ONE):
+        self.F, self.G, self.Pint = Fq28(P, ninv, fold_recip), Fr29(R), P
+        self.ONE = ONE
+        self.is_zero_mod, self.madd, self.mmadd, self.to_words = _fq28_formulas(self.F, B16, B32, B512, ONE)
+
+    def __call__(self, op, cases):
+        import numpy as np
+        out = np.zeros((len(cases), 48), dtype=np.uint64)
+        F, G = self.F, self.G
+        for i, x in enumerate(cases):
+            x = [list(v) for v in x] + [[0] * 16] * (5 - len(x))
+            a, b, c, d, e = (v[:14] for v in x)
+            if op == 0:
+                r = F.mul(a, b)
+            elif op == 1:
+                r = F.sqr(a)
+            elif op == 2:
+                r = F.mul2(a, b, c, d)
+            elif op == 3:
+                r = F.fold(a)
+            elif op == 4:
+                r = self.to_words(a, self.Pint)
+            elif op == 5:
+                r = F.carry(a)
+            elif op == 6:
+                r = [1 if self.is_zero_mod(a) else 0]
+            elif op == 7:
+                X, Y, Z = self.madd((a, b, c), d, e)
+                r = X + Y + Z
+            elif op == 8:
+                res = self.mmadd((a, b, None), d, e)
+                r = [0] * 42 + [0] if res is None else res[0] + res[1] + res[2] + [1]
+                if res is None:  # acc untouched
+                    r = a + b + list(self.ONE) + [0]
+            elif op == 20:
+                r = G.mul(x[0][:9], x[1][:9])
+            elif op == 21:
+                w = sum(int(v) << (32 * j) for j, v in enumerate(x[0][:8]))
+                r = [(w >> (29 * j)) & G.MASK for j in range(8)] + [w >> 232]
+            elif op == 22:
+                v = sum(int(t) << (29 * j) for j, t in enumerate(x[0][:9]))
+                r = [(v >> (32 * j)) & 0xffffffff for j in range(8)]
+            elif op == 23:
+                w = sum(int(v) << (32 * j) for j, v in enumerate(x[0][:8]))
+                m = G.mul([(w >> (29 * j)) & G.MASK for j in range(8)] + [w >> 232], x[1][:9])
+                v = sum(int(t) << (29 * j) for j, t in enumerate(m))
+                if v >= 1 << 256:
+                    raise Overflow("mul_words: product >= 2^256 does not pack")
+                r = [(v >> (32 * j)) & 0xffffffff for j in range(8)]
+            else:
+                raise ValueError(op)
+            out[i, :len(r)] = r
+        return out
