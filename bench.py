@@ -785,14 +785,24 @@ def cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, ntt_in, c
             ts.append(time.perf_counter() - t0)
         return statistics.median(ts), len(ts)
 
-    ref = H.oracle_msm("g1", s_std, b, threads=threads)
-    msm_s, runs = med(lambda: H.oracle_msm("g1", s_std, b, threads=threads), 5, args.cpu_budget_s)
     got = gpu_helpers.decode_icicle("g1", amd.to_numpy_u64(headline_result)[0])
+    # the baseline: the BLST-shaped Pippenger (signed digits, XYZZ buckets, window-parallel:
+    # orc_g1_msm_fast); the checker's plain restatement timed beside it
+    ref = H.oracle_msm("g1", s_std, b, threads=threads, fast=True)
+    msm_s, runs = med(lambda: H.oracle_msm("g1", s_std, b, threads=threads, fast=True), 5, args.cpu_budget_s)
     bit_exact = got == H.g1_from_affine_mont(ref)
+    ref_c = H.oracle_msm("g1", s_std, b, threads=threads)
+    chk_s, chk_runs = med(lambda: H.oracle_msm("g1", s_std, b, threads=threads), 3, args.cpu_budget_s)
     out = {"value": round(1.0 / msm_s, 4), "unit": "MSM/s", "cores": threads, "kind": "port",
            "sample": f"full G1 MSM of 2^{args.msm_log} points on the headline's inputs, median of {runs} runs after "
-                     f"one warmup, oracle/bls12_381_oracle.c OpenMP Pippenger on {threads} threads; BLST not available",
-           "bit_exact": bool(bit_exact)}
+                     f"one warmup, oracle/bls12_381_oracle.c orc_g1_msm_fast (BLST-shaped: signed c-bit digits, "
+                     f"XYZZ buckets, windows split evenly over {threads} OpenMP threads, C __int128 Montgomery "
+                     f"products); BLST itself is not available (no network, not in the image)",
+           "bit_exact": bool(bit_exact),
+           "checker_port_msm_per_sec": round(1.0 / chk_s, 4), "checker_port_runs": chk_runs,
+           "checker_port_bit_exact": bool(got == H.g1_from_affine_mont(ref_c)),
+           "checker_port_note": "the oracle's plain restatement (orc_g1_msm: unsigned windows, Jacobian buckets, "
+                                "points split over threads), the round-5 baseline"}
     # NTT (config #2 / the metric's second half): oracle radix-2 best_fft, all threads
     xn = np.ascontiguousarray(amd.to_numpy_u64(ntt_in))
     for log_n in (20, args.ntt_log):
@@ -820,7 +830,7 @@ def cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, ntt_in, c
         g2sn = np.ascontiguousarray(amd.to_numpy_u64(g2s))
         g2bn = np.ascontiguousarray(amd.to_numpy_u64(g2b))
         del g2s, g2b
-        t, runs = med(lambda: H.oracle_msm("g2", g2sn, g2bn, threads=threads), 5)
+        t, runs = med(lambda: H.oracle_msm("g2", g2sn, g2bn, threads=threads, fast=True), 5)
         out[f"g2_msm_2^{args.msm_log}_ms"] = round(t * 1e3, 1)
         out["g2_msm_runs"] = runs
         del g2sn, g2bn
@@ -837,7 +847,7 @@ def cpu_baseline(args, amd, torch, scalars, bases, n, headline_result, ntt_in, c
         del b4
         torch.cuda.empty_cache()
         t0 = time.perf_counter()
-        r4 = H.oracle_msm("g1", s4n, b4n, threads=threads)
+        r4 = H.oracle_msm("g1", s4n, b4n, threads=threads, fast=True)
         t4 = time.perf_counter() - t0
         got4 = gpu_helpers.decode_icicle("g1", amd.to_numpy_u64(cfg4_result)[0])
         out[f"g1_msm_2^{args.msm_total_log}_ms"] = round(t4 * 1e3, 1)

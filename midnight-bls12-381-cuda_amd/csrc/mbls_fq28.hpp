@@ -104,6 +104,19 @@ MBLS_DEV void mul2_cols(uint64_t& acc, uint32_t (&m)[NL], F28& r, const F28& a, 
         mul2_cols<K + 1>(acc, m, r, a, b, c, d);
     }
 }
+// four products, one reduction: a lane's share of a pair-sliced Fq2 product sum (mbls_fq2_28.hpp)
+template <int K>
+MBLS_DEV void mul4_cols(uint64_t& acc, uint32_t (&m)[NL], F28& r, const F28 (&x)[8]) {
+    if constexpr (K < 2 * NL - 1) {
+        constexpr int LO = K > NL - 1 ? K - (NL - 1) : 0, HI = K < NL - 1 ? K : NL - 1;
+        madc::col<K, LO, HI, false>(acc, x[0].l, x[1].l);
+        madc::col<K, LO, HI, false>(acc, x[2].l, x[3].l);
+        madc::col<K, LO, HI, false>(acc, x[4].l, x[5].l);
+        madc::col<K, LO, HI, false>(acc, x[6].l, x[7].l);
+        reduce_col<K>(acc, m, r);
+        mul4_cols<K + 1>(acc, m, r, x);
+    }
+}
 template <int K>
 MBLS_DEV void sqr_cols(uint64_t& acc, uint32_t (&m)[NL], F28& r, const F28& a, const uint32_t (&d)[NL]) {
     if constexpr (K < 2 * NL - 1) {
@@ -130,6 +143,18 @@ MBLS_DEV F28 mul2(const F28& a, const F28& b, const F28& c, const F28& d) {
     F28 r;
     uint64_t acc = 0;
     mul2_cols<0>(acc, m, r, a, b, c, d);
+    r.l[NL - 1] = (uint32_t)acc;
+    return r;
+}
+
+// a b + c d + e f + g h with one reduction (column bound: 56 products + 14 reduction terms)
+MBLS_DEV F28 mul4(const F28& a, const F28& b, const F28& c, const F28& d, const F28& e, const F28& f, const F28& g,
+                  const F28& h) {
+    uint32_t m[NL];
+    F28 r;
+    uint64_t acc = 0;
+    const F28 x[8] = {a, b, c, d, e, f, g, h};
+    mul4_cols<0>(acc, m, r, x);
     r.l[NL - 1] = (uint32_t)acc;
     return r;
 }

@@ -36,6 +36,7 @@
 #include "mbls_common.hpp"
 #include "mbls_curve.hpp"
 #include "mbls_fq28.hpp"
+#include "mbls_fq2_28.hpp"
 #include "mbls_rowfield.hpp"
 #include "mbls_wavepoint.hpp"
 
@@ -443,6 +444,97 @@ __global__ __launch_bounds__(256, MBLS_ACC_R28_MINW) void k_accumulate_r28(const
         vn = vnn;
     }
     store_jac28(partials, seg, acc);
+}
+
+// ------------------------------------------------------------------------------------
+// 4''. G2 accumulation in pair-sliced radix 2^28 (mbls_fq2_28.hpp; round 6).  k_accumulate's
+//     schedule over PAIRS of lanes (lane j: component j of every Fq2 value), with the next point
+//     prefetched into registers one addition ahead, the chunk's first point free and its second
+//     by mmadd; each lane's Fq2 product is one radix-2^28 product sum (no carry tracking).  The
+//     rare exceptional step (H = 0: equal or opposite points) converts the accumulator to words
+//     and takes jac_madd over PFq2.  Partials are stored in the library's canonical words: every
+//     other kernel is unchanged, and the partials equal k_accumulate<Fq2>'s bit for bit.
+// ------------------------------------------------------------------------------------
+#ifndef MBLS_ACC_G2_R28
+#define MBLS_ACC_G2_R28 1
+#endif
+#ifndef MBLS_ACC_G2_MINW
+#define MBLS_ACC_G2_MINW 2  // waves per SIMD the register budget is sized for
+#endif
+MBLS_DEV void store_jac28p(uint8_t* __restrict__ partials, uint32_t seg, const r28p::J28p& acc) {
+    Jacobian<PFq2> out;
+    if (acc.is_inf())
+        out = Jacobian<PFq2>::inf();
+    else
+        out = {r28p::to_pf(acc.x), r28p::to_pf(acc.y), r28p::to_pf(acc.z)};
+    store_jac<PFq2>(partials, seg, out);
+}
+
+template <class F>  // F = Fq2 only (a template so only msm_g2.hip instantiates it)
+__global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_accumulate_r28p(const uint32_t* __restrict__ sorted,
+                                                            const uint32_t* __restrict__ offsets,
+                                                            const uint32_t* __restrict__ chunk_off,
+                                                            const uint32_t* __restrict__ first, uint32_t b0,
+                                                            uint32_t b1, const uint8_t* __restrict__ bases,
+                                                            const uint8_t* __restrict__ phi, uint32_t nsplit,
+                                                            uint32_t chunk, uint8_t* __restrict__ partials) {
+    const uint32_t gb = offsets[b0], ge = offsets[b1];
+    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / 2 + gb / chunk;  // chunk index (pair)
+    uint32_t beg = t * chunk;
+    const uint32_t end = min(beg + chunk, ge);
+    beg = max(beg, gb);
+    if (beg >= end) return;  // pair-uniform: both lanes share t
+    uint32_t b = first[t];
+    while (offsets[b + 1] <= beg) ++b;
+    uint32_t seg = chunk_off[b] + (t - offsets[b] / chunk);
+    uint32_t bend = offsets[b + 1];
+    r28p::J28p acc = r28p::J28p::inf();
+    auto fetch = [&](uint32_t vv) {
+        uint32_t idx = vv >> 1;
+        const uint8_t* src = idx >= nsplit ? phi : bases;
+        idx = idx >= nsplit ? idx - nsplit : idx;
+        return load_affine<PFq2>(src, idx);  // this lane's component of x and y
+    };
+    uint32_t v = sorted[beg];
+    Affine<PFq2> p = fetch(v);
+    for (uint32_t e = beg; e < end; ++e) {
+        const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
+        const Affine<PFq2> pn = fetch(vn);  // one point ahead: the gather overlaps this addition
+        if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
+            store_jac28p(partials, seg, acc);
+            acc = r28p::J28p::inf();
+            do {
+                ++b;
+            } while (offsets[b + 1] == e);
+            seg = chunk_off[b];
+            bend = offsets[b + 1];
+        }
+        if (!p.is_inf()) {  // the affine identity (0, 0) adds nothing (pair-uniform predicate)
+            const r28::F28 qx = r28::unpack_shift8(p.x.v.v);
+            r28::F28 qy = r28::unpack_shift8(p.y.v.v);
+            if (v & 1) qy = r28::carry(r28::neg<r28::B512>(qy));  // -P, normalised (mbls_fq2_28.hpp)
+            if (acc.is_inf()) {
+                acc = {r28::fold(qx), r28::fold(qy), r28p::one()};
+            } else {
+                bool done = false;
+                if (MBLS_ACC_MMADD && e == beg + 1) done = r28p::mmadd(acc, qx, qy);
+                if (!done) done = r28p::madd(acc, qx, qy);
+                if (!done) {  // H = 0: doubling or the identity, in words (rare)
+                    const Jacobian<PFq2> aw = jac_madd(
+                        Jacobian<PFq2>{r28p::to_pf(acc.x), r28p::to_pf(acc.y), r28p::to_pf(acc.z)},
+                        (v & 1) ? aff_neg(p) : p);
+                    if (aw.is_inf())
+                        acc = r28p::J28p::inf();
+                    else
+                        acc = {r28::fold(r28p::from_pf(aw.x)), r28::fold(r28p::from_pf(aw.y)),
+                               r28::fold(r28p::from_pf(aw.z))};
+                }
+            }
+        }
+        v = vn;
+        p = pn;
+    }
+    store_jac28p(partials, seg, acc);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1339,9 +1431,10 @@ using AccKernel = void (*)(const uint32_t*, const uint32_t*, const uint32_t*, co
                            const uint8_t*, const uint8_t*, uint32_t, uint32_t, uint8_t*);
 template <class F>
 inline AccKernel accumulate_kernel() {
-    if (std::is_same<F, Fq>::value && MBLS_ACC_R28 && MBLS_ACC_LDS) return k_accumulate_r28<F>;
-    if (std::is_same<F, Fq>::value && MBLS_ACC_W3) return k_accumulate<F, 3>;
-    return k_accumulate<F, 1>;
+    if constexpr (std::is_same<F, Fq>::value && MBLS_ACC_R28 && MBLS_ACC_LDS) return k_accumulate_r28<F>;
+    else if constexpr (std::is_same<F, Fq2>::value && MBLS_ACC_G2_R28) return k_accumulate_r28p<F>;
+    else if constexpr (std::is_same<F, Fq>::value && MBLS_ACC_W3) return k_accumulate<F, 3>;
+    else return k_accumulate<F, 1>;
 }
 
 // contributions per accumulation thread: CHUNK (16), or an eighth of the average bucket when

@@ -49,9 +49,6 @@ namespace mbls {
 #ifndef MBLS_NTT_THREADS
 #define MBLS_NTT_THREADS 256
 #endif
-#ifndef MBLS_NTT_WAVES
-#define MBLS_NTT_WAVES 4  // resident workgroups per CU (grid = CUs x this; <= 5, the LDS bound of 32 KiB tiles)
-#endif
 #ifndef MBLS_NTT_XCD
 #define MBLS_NTT_XCD 0  // 1: tiles of adjacent columns on the same XCD (shared L2 lines)
 #endif
@@ -80,7 +77,6 @@ static const uint64_t ROOT_2_32_MONT[4] = {0xb9b58d8c5f0e466aULL, 0x5b1b4c801819
 struct DomainTables {
     int max_log = 0;            // stage tables built for stages 1..max_log
     uint32_t count = 0;         // entries per table (2^max_log - 1): the limb planes' stride
-    int cus = 0;                // compute units of `device` (the passes' resident workgroups)
     int device = 0;             // device the tables live on
     uint8_t* tw = nullptr;      // per-stage w_(2^s)^i tables (see header)
     uint8_t* tw_inv = nullptr;  // per-stage w_(2^s)^-i
@@ -207,11 +203,10 @@ MBLS_DEV r29::F29 ldtw(const uint4* a, const uint4* b, const uint32_t* c, uint32
 // One pass of up to NTT_TILE_LOG DIT stages.
 //   FIRST: stages 1..L with the bit-reversal gather from `in`; else stages s0+1..s0+L in place.
 //   LAST:  store canonical values; SCALE (inverse, implies LAST): multiply them by n^-1.
-// Persistent workgroups: the grid is at most the resident workgroup count (ntt_device) and each
-// workgroup walks tiles id, id + grid, ...: a workgroup goes from storing one tile straight to
-// loading the next, so its stores drain behind the next tile's load and arithmetic instead of
-// holding the workgroup slot (one tile per workgroup, round 5: the loads cost 7.5% and the stores
-// 8% of the transform, profiles/r06/ntt_phases.txt).
+// One tile per workgroup, grid = tiles.  (Persistent workgroups walking several tiles were
+// measured 11% SLOWER, round 6: on gfx9 vmcnt counts loads and stores in one in-order counter, so
+// the first wait on the next tile's loads -- or on a twiddle load -- also waits for this tile's
+// stores, while a fresh workgroup starts with no stores outstanding; profiles/r06/README.md.)
 // Index arithmetic is 32-bit (element indices inside a polynomial and the twiddle tables stay
 // below 2^31 for transforms <= 2^30), the tile is a uint4 LDS array (every access one b128),
 // and the 2r constants are literals (the pass is VALU-issue bound, profiles/r05/ntt_diag.txt).
@@ -252,10 +247,12 @@ __global__ __launch_bounds__(NTT_THREADS, 5) void k_ntt_pass(uint8_t* __restrict
     const uint4* in = reinterpret_cast<const uint4*>(FIRST ? in_ : out_);
     uint4* out = reinterpret_cast<uint4*>(out_);
 
-    for (uint32_t id = blockIdx.x; id < ntiles; id += gridDim.x) {
-        const Tile g = tile_of(id);
-        // ---- the tile into LDS as [row t][col c] (FIRST: rows at their bit-reversed DIT position)
-        // (not vectorised: the loop vectoriser split the b128 LDS stores into ds_write_b32)
+    const uint32_t id = blockIdx.x;  // one tile per workgroup
+    if (id >= ntiles) return;
+    const Tile g = tile_of(id);
+    {
+        // ---- the tile into LDS as [row t][col c] (FIRST: rows at their bit-reversed DIT
+        // position; not vectorised: the loop vectoriser split the b128 LDS stores into b32)
 #pragma clang loop vectorize(disable) interleave(disable)
         for (uint32_t e = threadIdx.x; e < T; e += NTT_THREADS) {
             const uint32_t c = e & (C - 1), t = e >> logC;
@@ -266,7 +263,6 @@ __global__ __launch_bounds__(NTT_THREADS, 5) void k_ntt_pass(uint8_t* __restrict
             }
         }
         __syncthreads();
-
         // ---- L DIT stages: pairs of stages as radix-4 (2 x 2) butterflies in registers (one LDS
         // round trip and one barrier per pair), an odd last stage as radix-2
         const uint32_t lo_base = FIRST ? 0u : g.lo0;
@@ -351,7 +347,6 @@ __global__ __launch_bounds__(NTT_THREADS, 5) void k_ntt_pass(uint8_t* __restrict
             if (MBLS_NTT_EXP == 4 && (v.v[0] ^ v.v[7]) != 0x12345u) continue;  // (almost) never stores
             st2(o, dst, v);
         }
-        __syncthreads();  // every read of this tile done before the next one is written
     }
 }
 
@@ -472,7 +467,6 @@ static eIcicleError build_domain(Domain& dom, int max_log, hipStream_t st, std::
     MBLS_TRY(hipMalloc(&t->tw, TW_ENTRY_BYTES * count));
     MBLS_TRY(hipMalloc(&t->tw_inv, TW_ENTRY_BYTES * count));
     t->count = (uint32_t)count;
-    MBLS_TRY(hipDeviceGetAttribute(&t->cus, hipDeviceAttributeMultiprocessorCount, t->device));
     uint64_t w[4], wi[4];
     canonical_omega(w, max_log);
     hfr_inv(wi, w);
@@ -524,11 +518,8 @@ eIcicleError ntt_device(uint8_t* out, const uint8_t* in, int log_n, bool inverse
         if (logC > colspace) logC = colspace;
         size_t tiles = (n >> (L + logC)) * (size_t)batch;
         if (tiles > 0x7fffffff) return MBLS_INVALID_ARGUMENT;
-        // persistent workgroups: at most the resident count (one per SIMD-wave slot the pass is
-        // compiled for), each walking tiles id, id + grid, ...
-        const size_t resident = (size_t)(D.cus > 0 ? D.cus : 256) * MBLS_NTT_WAVES;
         const uint32_t nt = (uint32_t)tiles;
-        dim3 grid((unsigned)(tiles < resident ? tiles : resident)), blk(NTT_THREADS);
+        dim3 grid(nt), blk(NTT_THREADS);
         if (first && last && inverse)
             hipLaunchKernelGGL((k_ntt_pass<true, true, true>), grid, blk, 0, st, out, in, tw, D.count, log_n, s0, L, logC, scale, nt);
         else if (first && last)

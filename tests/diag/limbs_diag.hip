@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "mbls_fq28.hpp"
+#include "mbls_fq2_28.hpp"
 #include "mbls_fr29.hpp"
 
 using namespace mbls;
@@ -39,6 +40,8 @@ MBLS_DEV r29::F29 f29(const uint32_t* p) {
 //         5 carry(x0)   6 is_zero_mod(x0) (1 word)   7 madd(acc = x0, x1, x2; q = x3, x4): 42 words
 //         8 mmadd(acc = x0, x1, one; q = x3, x4): 42 words + the flag
 //  r29: 20 mul(x0, x1)   21 unpack(words x0)   22 pack(x0) (8 words)   23 mul_words(words x0, x1)
+//  pair-sliced Fq2 (mbls_fq2_28.hpp): rows 2i, 2i + 1 are the two lanes of case i (component 0, 1):
+//       30 madd(acc = x0, x1, x2; q = x3, x4): 42 words + the flag   31 mmadd(acc = x0, x1; q = x3, x4)
 __global__ void k_limbs(int op, const uint32_t* __restrict__ in, uint32_t* __restrict__ out, int n) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
@@ -96,6 +99,16 @@ __global__ void k_limbs(int op, const uint32_t* __restrict__ in, uint32_t* __res
             for (int i = 0; i < 8; ++i) a.v[i] = x[i];
             const Fr r = r29::mul_words(a, f29(x + 16));
             for (int i = 0; i < 8; ++i) o[i] = r.v[i];
+            break;
+        }
+        case 30:
+        case 31: {
+            r28p::J28p acc{f28(x), f28(x + 16), op == 30 ? f28(x + 32) : r28p::one()};
+            const bool done = op == 30 ? r28p::madd(acc, f28(x + 48), f28(x + 64)) : r28p::mmadd(acc, f28(x + 48), f28(x + 64));
+            put28(o, acc.x);
+            put28(o + 14, acc.y);
+            put28(o + 28, acc.z);
+            o[42] = done ? 1u : 0u;
             break;
         }
         default: o[0] = 0xdeadbeefu; break;

@@ -114,7 +114,7 @@ def oracle():
         getattr(lib, nm).argtypes = [P, P, P, sz]
     lib.orc_omega.argtypes = [P, ctypes.c_int]
     lib.orc_ntt.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
-    for nm in ("orc_g1_msm", "orc_g2_msm"):
+    for nm in ("orc_g1_msm", "orc_g2_msm", "orc_g1_msm_fast", "orc_g2_msm_fast"):
         getattr(lib, nm).argtypes = [P, P, P, sz, ctypes.c_int]
         getattr(lib, nm).restype = ctypes.c_int
     lib.orc_gen_scalars.argtypes = [P, ctypes.c_uint64, sz]
@@ -132,11 +132,16 @@ def ptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def oracle_msm(group, scalars_std: np.ndarray, bases_mont: np.ndarray, threads=0):
+def oracle_msm(group, scalars_std: np.ndarray, bases_mont: np.ndarray, threads=0, fast=False):
+    """fast: the window-parallel XYZZ Pippenger (orc_g*_msm_fast, the bench's CPU baseline) instead of
+    the checker's restatement"""
     lib = oracle()
     n = scalars_std.shape[0]
     out = np.zeros(12 if group == "g1" else 24, dtype=np.uint64)
-    fn = lib.orc_g1_msm if group == "g1" else lib.orc_g2_msm
+    if fast:
+        fn = lib.orc_g1_msm_fast if group == "g1" else lib.orc_g2_msm_fast
+    else:
+        fn = lib.orc_g1_msm if group == "g1" else lib.orc_g2_msm
     fn(ptr(out), ptr(np.ascontiguousarray(scalars_std)), ptr(np.ascontiguousarray(bases_mont)), n, threads)
     return out
 

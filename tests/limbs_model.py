@@ -16,9 +16,14 @@ class Overflow(AssertionError):
     pass
 
 
+PEAK = {}  # largest column accumulator seen per operation (the bound tables' margins)
+
+
 def _chk64(acc, what):
     if not 0 <= acc < U64:
         raise Overflow(f"{what}: column accumulator {acc:#x} >= 2^64")
+    if acc > PEAK.get(what, 0):
+        PEAK[what] = acc
     return acc
 
 
@@ -267,6 +272,8 @@ class Model:
                 r = [0] * 42 + [0] if res is None else res[0] + res[1] + res[2] + [1]
                 if res is None:  # acc untouched
                     r = a + b + list(self.ONE) + [0]
+            elif op in (30, 31):
+                raise ValueError("pair ops: use run_pairs")
             elif op == 20:
                 r = G.mul(x[0][:9], x[1][:9])
             elif op == 21:
@@ -286,3 +293,113 @@ class Model:
                 raise ValueError(op)
             out[i, :len(r)] = r
         return out
+
+
+# ------------------------------------------------------------------ pair-sliced Fq2 (mbls_fq2_28.hpp)
+class Fq2P28:
+    """lane j of a pair holds component c_j (14 limbs); the partner's limbs arrive by DPP.  Every
+    operation here is what ONE pair of lanes computes, lane 0 and lane 1 each with the model F."""
+
+    def __init__(self, F, B16, B32, B512):
+        self.F, self.B16, self.B32, self.B512 = F, B16, B32, B512
+
+    def mul4(self, terms):
+        """sum of up to 4 limb products with ONE reduction (a lane's share of an Fq2 product or
+        product sum); the column bound covers all of them at once"""
+        F = self.F
+        NL = F.NL
+        for a, b in terms:
+            for v in a + b:
+                _chk32(v, "operand")
+        m, r, acc = [0] * NL, [0] * NL, 0
+        for k in range(2 * NL - 1):
+            lo, hi = (k - (NL - 1) if k > NL - 1 else 0), (k if k < NL - 1 else NL - 1)
+            for a, b in terms:
+                for i in range(lo, hi + 1):
+                    acc = _chk64(acc + a[i] * b[k - i], "fq2 product")
+            acc = F._reduce_col(acc, m, r, k, "fq2 reduction")
+        r[NL - 1] = _chk32(acc, "fq2 top limb")
+        return r
+
+    def mul(self, a, b, bk):
+        """a b: lane 0 a0 b0 + a1 (bk - b1), lane 1 a1 b0 + a0 b1; bk: the bias of the partner
+        negation (limbs >= b1's)"""
+        F = self.F
+        return (self.mul4([(a[0], b[0]), (a[1], F.neg(bk, b[1]))]), self.mul4([(a[1], b[0]), (a[0], b[1])]))
+
+    def mul2(self, a, b, c, d, bkb, bkd):
+        F = self.F
+        return (self.mul4([(a[0], b[0]), (a[1], F.neg(bkb, b[1])), (c[0], d[0]), (c[1], F.neg(bkd, d[1]))]),
+                self.mul4([(a[1], b[0]), (a[0], b[1]), (c[1], d[0]), (c[0], d[1])]))
+
+    def sqr(self, a, bk):
+        """lane 0 (a0 + a1)(a0 - a1 + bk), lane 1 a1 (2 a0)"""
+        F = self.F
+        return (self.mul4([(F.add(a[0], a[1]), F.sub(bk, a[0], a[1]))]), self.mul4([(a[1], F.x2(a[0]))]))
+
+    def each(self, f, *xs):
+        return tuple(f(*(x[j] for x in xs)) for j in range(2))
+
+
+def _fq2_formulas(F, B16, B32, B512, ONE):
+    """the G2 accumulation's madd / mmadd over pair-sliced radix-2^28 Fq2, with the carries that
+    keep every product's columns below 2^64 (csrc/mbls_fq2_28.hpp follows this step for step)"""
+    Q = Fq2P28(F, B16, B32, B512)
+    ONE2 = (list(ONE), [0] * 14)
+    e = Q.each
+
+    Pint = sum(v << (28 * i) for i, v in enumerate(F.P))
+
+    def is_zero_lt2p(a):
+        """0 mod p for components below 2p (the test reads 0 or p): asserts that precondition"""
+        for c in a:
+            if sum(v << (28 * i) for i, v in enumerate(c)) >= 2 * Pint:
+                raise Overflow("is_zero_lt2p: component >= 2p")
+        P = F.P
+        return all(all(v == 0 for v in c) or c == P for c in a)
+
+    def madd(acc, x2_, y2_):
+        """acc (x, y normalised < 3p, z normalised); q = (x2_, y2_) normalised (the caller
+        carries a negated y2).  None for the exceptional H = 0 (the kernel's word-form path).
+        The partner negations take the bias whose limbs (top limb included) cover the operand:
+        B16 for values < 16p, B32 < 32p, B512 beyond."""
+        x, y, z = acc
+        Z1Z1 = Q.sqr(z, B16)
+        U2 = Q.mul(x2_, Z1Z1, B16)
+        S2 = Q.mul(Q.mul(y2_, z, B16), Z1Z1, B16)
+        H = e(F.carry, e(lambda a, b: F.sub(B16, a, b), U2, x))  # < 19p
+        R = e(lambda a, b: F.sub(B16, a, b), S2, y)
+        HH = Q.sqr(H, B32)
+        if is_zero_lt2p(HH):
+            return None
+        I = e(F.x4, HH)
+        J = Q.mul(H, I, B512)
+        Z3 = Q.mul(e(F.x2, z), H, B32)
+        V = Q.mul(x, I, B512)
+        R2 = e(F.carry, e(F.x2, R))  # < 38p
+        X3 = e(F.fold, e(lambda a, b: F.sub(B32, a, b), e(lambda a, b: F.sub(B16, a, b), Q.sqr(R2, B512), J),
+                         e(F.x2, V)))
+        VX = e(F.carry, e(lambda a, b: F.sub(B16, a, b), V, X3))  # < 19p
+        NY = e(F.carry, e(lambda a: F.neg(B32, a), e(F.x2, y)))
+        Y3 = Q.mul2(R2, VX, NY, J, B32, B16)
+        return X3, Y3, Z3
+
+    def mmadd(acc, x2_, y2_):
+        x, y, _ = acc
+        H = e(F.fold, e(lambda a, b: F.sub(B512, a, b), x2_, x))
+        HH = Q.sqr(H, B16)
+        if is_zero_lt2p(HH):
+            return None
+        I = e(F.x4, HH)
+        J = Q.mul(H, I, B512)
+        Z3 = e(F.carry, e(F.x2, H))
+        V = Q.mul(x, I, B512)
+        R2 = e(F.carry, e(F.x2, e(F.fold, e(lambda a, b: F.sub(B512, a, b), y2_, y))))
+        X3 = e(F.fold, e(lambda a, b: F.sub(B32, a, b), e(lambda a, b: F.sub(B16, a, b), Q.sqr(R2, B16), J),
+                         e(F.x2, V)))
+        VX = e(F.carry, e(lambda a, b: F.sub(B16, a, b), V, X3))
+        NY = e(F.carry, e(lambda a: F.neg(B32, a), e(F.x2, y)))
+        Y3 = Q.mul2(R2, VX, NY, J, B32, B16)
+        return X3, Y3, Z3
+
+    return madd, mmadd

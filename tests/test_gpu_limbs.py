@@ -105,7 +105,7 @@ def diag(request):
 
 rng = random.Random(0x1F28)
 FQ28 = open(os.path.join(CSRC, "mbls_fq28.hpp")).read()
-B16, B32, B512 = (_carray(FQ28, n) for n in ("B16", "B32", "B512"))
+B16, B32, B512, ONE28 = (_carray(FQ28, n) for n in ("B16", "B32", "B512", "ONE"))
 
 
 def mm(a, b):  # radix-2^28 Montgomery product mod p
@@ -329,3 +329,112 @@ def test_model_detects_overflow():
     G = limbs_model.Fr29(R)
     with pytest.raises(limbs_model.Overflow):
         G.mul([(1 << 32) - 1] * 9, [(1 << 32) - 1] * 9)
+
+
+# ----------------------------------------------------------------------------- pair-sliced Fq2 (G2)
+def _fq2_ops():
+    inv = pow(RP28, -1, P)
+
+    def mm2(a, b):  # Fq2 Montgomery product (radix R' = 2^392), u^2 = -1
+        return ((a[0] * b[0] - a[1] * b[1]) * inv % P, (a[0] * b[1] + a[1] * b[0]) * inv % P)
+
+    def lin(*terms):  # sum of k * a over (k, a)
+        return tuple(sum(k * a[j] for k, a in terms) % P for j in range(2))
+    return mm2, lin
+
+
+def madd2_ref(X, Y, Z, x2v, y2v):
+    """jac_madd's Fq2 field values (madd-2007-bl, lazy Y3, Z3 = 2 Z1 H); None: H = 0"""
+    mm2, lin = _fq2_ops()
+    ZZ = mm2(Z, Z)
+    H = lin((1, mm2(x2v, ZZ)), (-1, X))
+    Rr = lin((1, mm2(mm2(y2v, Z), ZZ)), (-1, Y))
+    if H == (0, 0):
+        return None
+    I = lin((4, mm2(H, H)))
+    J, V, R2 = mm2(H, I), mm2(X, I), lin((2, Rr))
+    X3 = lin((1, mm2(R2, R2)), (-1, J), (-2, V))
+    Y3 = lin((1, mm2(R2, lin((1, V), (-1, X3)))), (-2, mm2(Y, J)))
+    return X3, Y3, mm2(lin((2, Z)), H)
+
+
+def _v2(a):
+    return (_val(a[0], 28) % P, _val(a[1], 28) % P)
+
+
+def fq2_madd_cases():
+    """accumulators at their invariant bounds (x, y normalised < 3p, z normalised), bases at the
+    unpack extremes with the negated y carried (the kernel's form), per component"""
+    import limbs_model
+    F = limbs_model.Fq28(P, 0xffcfffd, (1 << 40) // (0x1a011 + 1))
+    xs = [norm_max(3 * P), _limbs(3 * P - 1, 28, 14), _limbs(P, 28, 14), _limbs(rng.randrange(3 * P), 28, 14)]
+    zs = [norm_max(6 * P), _limbs(2 * P - 1, 28, 14), _limbs(rng.randrange(6 * P), 28, 14)]
+    q = [unpack8(P - 1), unpack8(0), unpack8(rng.randrange(P))]
+    cases = []
+    for k in range(48):
+        X = (xs[k % 4], xs[(k // 4) % 4])
+        Y = (xs[(k + 1) % 4], xs[(k // 2) % 4])
+        Z = (zs[k % 3], zs[(k // 3) % 3])
+        qx = (q[k % 3], q[(k + 1) % 3])
+        qy = (q[(k // 3) % 3], q[(k + 2) % 3])
+        if k % 2:  # negative digit: y2 = carry(neg<B512>(qy)) per component
+            qy = tuple(F.carry(F.neg(B512, c)) for c in qy)
+        cases.append((X, Y, Z, qx, qy))
+    return cases
+
+
+def test_fq2_pair_madd_model():
+    """the pair-sliced radix-2^28 G2 mixed additions (tests/limbs_model.py _fq2_formulas, what
+    csrc/mbls_fq2_28.hpp computes): no column reaches 2^64, every coordinate equals jac_madd's
+    field value, outputs keep the accumulator invariant"""
+    import limbs_model
+    src = open(os.path.join(CSRC, "mbls_fq28.hpp")).read()
+    F = limbs_model.Fq28(P, 0xffcfffd, (1 << 40) // (0x1a011 + 1))
+    madd, mmadd = limbs_model._fq2_formulas(F, B16, B32, B512, _carray(src, "ONE"))
+    for i, (X, Y, Z, qx, qy) in enumerate(fq2_madd_cases()):
+        r = madd((X, Y, Z), qx, qy)
+        exp = madd2_ref(_v2(X), _v2(Y), _v2(Z), _v2(qx), _v2(qy))
+        assert (r is None) == (exp is None), i
+        if r is None:
+            continue
+        assert tuple(_v2(c) for c in r) == exp, ("g2 madd", i)
+        for c in r[0] + r[1] + r[2]:
+            assert is_normalised(c)
+        assert all(_val(c, 28) < 3 * P for c in r[0] + r[1]) and all(_val(c, 28) < 6 * P for c in r[2])
+        one = (RP28 % P, 0)
+        r = mmadd((X, Y, None), qx, qy)
+        exp = madd2_ref(_v2(X), _v2(Y), one, _v2(qx), _v2(qy))
+        assert tuple(_v2(c) for c in r) == exp, ("g2 mmadd", i)
+        for c in r[0] + r[1] + r[2]:
+            assert is_normalised(c)
+        assert all(_val(c, 28) < 3 * P for c in r[0] + r[1]) and all(_val(c, 28) < 6 * P for c in r[2])
+
+
+@pytest.mark.gpu
+def test_fq2_pair_madd_device(diag):
+    """the device's pair-sliced G2 madd / mmadd (csrc/mbls_fq2_28.hpp) on the model's cases:
+    every coordinate equals jac_madd's field value and the model's limbs, bit for bit"""
+    import limbs_model
+    src = open(os.path.join(CSRC, "mbls_fq28.hpp")).read()
+    F = limbs_model.Fq28(P, 0xffcfffd, (1 << 40) // (0x1a011 + 1))
+    madd, mmadd = limbs_model._fq2_formulas(F, B16, B32, B512, _carray(src, "ONE"))
+    cases = fq2_madd_cases()
+    # the exceptional H = 0 case: acc = q with another representative (the caller's word path)
+    X, Y, Z, qx, qy = cases[0]
+    cases.append(((unpack8(5), unpack8(7)), Y, ([int(v) for v in ONE28], [0] * 14), (unpack8(5), unpack8(7)), qy))
+    for op, fn in ((30, madd), (31, mmadd)):
+        rows = []
+        for X, Y, Z, qx, qy in cases:
+            for j in range(2):
+                rows.append([X[j], Y[j], Z[j], qx[j], qy[j]])
+        o = diag(op, rows)
+        for i, (X, Y, Z, qx, qy) in enumerate(cases):
+            exp = fn((X, Y, Z), qx, qy)
+            done = int(o[2 * i, 42])
+            assert done == int(o[2 * i + 1, 42]) == (0 if exp is None else 1), (op, i)
+            if exp is None:
+                continue
+            for k in range(3):
+                for j in range(2):
+                    got = [int(v) for v in o[2 * i + j, 14 * k:14 * k + 14]]
+                    assert got == exp[k][j], (op, i, k, j)
