@@ -38,7 +38,7 @@ PROFILES = os.path.join(ROOT, "profiles")
 
 
 def pmc_summary():
-    for rnd in ("r05/closing", "r04/closing", "r03", "r02", "r01"):
+    for rnd in ("r06/closing", "r05/closing", "r04/closing", "r03", "r02", "r01"):
         path = os.path.join(PROFILES, rnd, "pmc_summary.json")
         try:
             with open(path) as f:
@@ -84,7 +84,17 @@ def valu_issue_bound_ms(kernel, cyc_per_instr, mhz):
 CEILING_BIN = os.path.join(ROOT, "tools", "valu_ceiling")
 
 
+_CEILING = []
+
+
 def valu_ceiling():
+    """the measured ceilings, run once per bench process (main and the mix leg share them)"""
+    if not _CEILING:
+        _CEILING.append(_valu_ceiling())
+    return _CEILING[0]
+
+
+def _valu_ceiling():
     """Measured VALU ceilings (tools/valu_ceiling.hip): k_accumulate<G1>'s
     arithmetic (same madd / mmadd code, same 168-VGPR / 3-wave bounds, points from LDS) and
     k_ntt_pass's radix-4 body, register-resident.  Run live on this box as a child process when
@@ -99,7 +109,9 @@ def valu_ceiling():
                 return d
         except (OSError, ValueError, subprocess.TimeoutExpired):
             pass
-    path = os.path.join(PROFILES, "r05", "valu_ceiling.json")
+    path = os.path.join(PROFILES, "r06", "valu_ceiling.json")
+    if not os.path.exists(path):
+        path = os.path.join(PROFILES, "r05", "valu_ceiling.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -382,7 +394,8 @@ def main():
         ceil = valu_ceiling() or {}
         # G1's accumulation is k_accumulate_r28 (round 5): its own arithmetic's ceiling when measured
         acc_c = ceil.get("acc28_ceiling") or ceil.get("acc_ceiling") or {}
-        ntt_c = ceil.get("ntt_ceiling") or {}
+        # the shipped pass multiplies in radix 2^29 (round 6): its own body's ceiling when measured
+        ntt_c = ceil.get("ntt29_ceiling") or ceil.get("ntt_ceiling") or {}
         isa = ceil.get("isa_2") or {}
         cyc = isa.get("simd_cycles_per_wave_instr")
         # the ceiling's ns per contribution at this MSM's contribution count
@@ -449,8 +462,11 @@ def main():
                              "traffic": ntt_traffic(args.ntt_log),
                              "valu_ceiling_ms": round(ntt_ceiling_ms, 4) if ntt_ceiling_ms else None,
                              "valu_frac": round(ntt_ceiling_ms / ntt_ms, 4) if ntt_ceiling_ms and ntt_ms else None,
-                             "valu_ceiling_source": "microbench (k_ntt_ceiling: the pass's radix-4 body, "
-                                                    "register-resident, twiddles in LDS; stage pairs 2..11)",
+                             "valu_ceiling_source": "microbench (k_ntt29_ceiling: the shipped pass's radix-4 body -- "
+                                                    "radix-2^29 products, lazy [0, 2r) additions -- register-"
+                                                    "resident, twiddle limb planes in LDS; 10 stage pairs, i.e. "
+                                                    "the transform's 22 stages minus the first pair's trivial "
+                                                    "products)",
                              "counter_issue_ms": ntt_issue_ms,
                              "counter_issue_frac": round(ntt_issue_ms / ntt_ms, 4) if ntt_issue_ms and ntt_ms else None,
                              "pass_ms": round(ntt_pass_ms, 4) if ntt_pass_ms else None},
@@ -717,20 +733,26 @@ def mix_leg(args, amd, torch, dev, rank, timed):
     acc_ms = g2_stage_ms(amd, torch, dev, g2, s_a)
     contributions = 4 * n * ((64 + 16 - 1) // 16)  # psi split: 4n digit streams x 4 windows (c = 16)
     ceil = valu_ceiling() or {}
-    cyc = (ceil.get("isa_2") or {}).get("simd_cycles_per_wave_instr")
-    issue = valu_issue_bound_ms("k_accumulate<G2>", cyc, (ceil.get("acc_ceiling") or {}).get("mhz_med"))
+    g2c = ceil.get("acc28p_ceiling") or {}
+    g2_ceiling_ms = g2c["ms_per_2^20_g2_msm_contributions"] * contributions / 16777216.0 if g2c else None
     return {"g2_msm_points": n, "ntt_batch": B, "ntt_size": nn, "g2_msm_ms": round(g2_ms, 3),
             "g2_msm_per_sec": round(1e3 / g2_ms, 3),
             "g2_prepared_bases_ms": round(g2p_ms, 3), "g2_prepared_equal_to_plain": g2p_same,
             "g2_roofline_hbm_frac": round(G2_BYTES_PER_POINT * n / (g2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
             "g2_accumulate_ms": round(acc_ms, 4) if acc_ms else None,
-            "g2_roofline_valu": {"kernel": "k_accumulate<G2> (pair-sliced Fq2 lanes)", "bound": "valu",
+            "g2_roofline_valu": {"kernel": "k_accumulate_r28p<G2> (pair-sliced radix-2^28 Fq2 lanes)", "bound": "valu",
                                  "achieved": round(contributions / (acc_ms * 1e-3) / 1e9, 3) if acc_ms else None,
+                                 "peak": round(contributions / (g2_ceiling_ms * 1e-3) / 1e9, 3)
+                                 if g2_ceiling_ms else None,
                                  "unit": "G mixed additions/s",
-                                 "counter_issue_ms": round(issue, 4) if issue else None,
-                                 "counter_issue_frac": round(issue / acc_ms, 4) if issue and acc_ms else None,
-                                 "note": "counter_issue_ms = committed SQ_INSTS_VALU x the measured cycles per "
-                                         "wave-instruction (tools/valu_ceiling.hip) / 1024 SIMDs / measured clock"},
+                                 "frac": round(g2_ceiling_ms / acc_ms, 4) if g2_ceiling_ms and acc_ms else None,
+                                 "ceiling_ms": round(g2_ceiling_ms, 4) if g2_ceiling_ms else None,
+                                 "ceiling": g2c or None,
+                                 "ceiling_source": ceil.get("source", "live: tools/valu_ceiling") if g2c else None,
+                                 "note": f"{contributions} mixed additions per launch (psi split: 4n digit streams x 4 "
+                                         "windows); peak = k_acc28p_ceiling (tools/valu_ceiling.hip: the same "
+                                         "pair-sliced madd / mmadd and launch bounds with the points in LDS), "
+                                         "measured on the box; frac = ceiling time / kernel time"},
             "batched_ntt_ms": round(ntt_ms, 3), "overlapped_ms": round(both_ms, 3),
             "sum_isolated_ms": round(g2_ms + ntt_ms, 3), "streams": 2,
             "overlap_ratio": round(both_ms / (g2_ms + ntt_ms), 4),

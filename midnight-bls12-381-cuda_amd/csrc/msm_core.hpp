@@ -461,6 +461,9 @@ __global__ __launch_bounds__(256, MBLS_ACC_R28_MINW) void k_accumulate_r28(const
 #ifndef MBLS_ACC_G2_MINW
 #define MBLS_ACC_G2_MINW 2  // waves per SIMD the register budget is sized for
 #endif
+#ifndef MBLS_ACC_G2_LDS
+#define MBLS_ACC_G2_LDS 0  // 1: next point prefetched into LDS (LDS-DMA) instead of VGPRs
+#endif
 MBLS_DEV void store_jac28p(uint8_t* __restrict__ partials, uint32_t seg, const r28p::J28p& acc) {
     Jacobian<PFq2> out;
     if (acc.is_inf())
@@ -489,6 +492,39 @@ __global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_accumulate_r28p(const
     uint32_t seg = chunk_off[b] + (t - offsets[b] / chunk);
     uint32_t bend = offsets[b + 1];
     r28p::J28p acc = r28p::J28p::inf();
+#if MBLS_ACC_G2_LDS
+    // the next point's component (x: 3 x 16 B, y: 3 x 16 B per lane) prefetched into LDS by
+    // LDS-DMA, double-buffered per wave (the G1 kernel's stage): no 24 VGPRs held across the
+    // addition.  Stage: [slot][wave][piece][lane] x 16 B = 48 KiB per workgroup.
+    __shared__ uint4 stage[2][256 / 64][6][64];
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const uint32_t half = pairdpp::odd() ? 48u : 0u;
+    auto issue = [&](uint32_t vv, uint32_t slot) {
+        uint32_t idx = vv >> 1;
+        const uint8_t* src = idx >= nsplit ? phi : bases;
+        idx = idx >= nsplit ? idx - nsplit : idx;
+        const uint8_t* g = src + (size_t)idx * 192 + half;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(g + (k < 3 ? 16 * k : 96 + 16 * (k - 3))),
+                                             (__attribute__((address_space(3))) void*)&stage[slot][wv][k][0], 16, 0, 0);
+    };
+    uint32_t v = sorted[beg];
+    issue(v, 0);
+    uint32_t vn = beg + 1 < end ? sorted[beg + 1] : v;
+    for (uint32_t e = beg; e < end; ++e) {
+        const uint32_t slot = (e - beg) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this point's pieces have landed
+        Affine<PFq2> p;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint4 xa = stage[slot][wv][k][ln], ya = stage[slot][wv][3 + k][ln];
+            p.x.v.v[4 * k] = xa.x, p.x.v.v[4 * k + 1] = xa.y, p.x.v.v[4 * k + 2] = xa.z, p.x.v.v[4 * k + 3] = xa.w;
+            p.y.v.v[4 * k] = ya.x, p.y.v.v[4 * k + 1] = ya.y, p.y.v.v[4 * k + 2] = ya.z, p.y.v.v[4 * k + 3] = ya.w;
+        }
+        if (e + 1 < end) issue(vn, slot ^ 1u);  // the other slot was read one addition ago
+        const uint32_t vnn = e + 2 < end ? sorted[e + 2] : vn;
+#else
     auto fetch = [&](uint32_t vv) {
         uint32_t idx = vv >> 1;
         const uint8_t* src = idx >= nsplit ? phi : bases;
@@ -500,6 +536,7 @@ __global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_accumulate_r28p(const
     for (uint32_t e = beg; e < end; ++e) {
         const uint32_t vn = e + 1 < end ? sorted[e + 1] : v;
         const Affine<PFq2> pn = fetch(vn);  // one point ahead: the gather overlaps this addition
+#endif
         if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
             store_jac28p(partials, seg, acc);
             acc = r28p::J28p::inf();
@@ -531,8 +568,13 @@ __global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_accumulate_r28p(const
                 }
             }
         }
+#if MBLS_ACC_G2_LDS
+        v = vn;
+        vn = vnn;
+#else
         v = vn;
         p = pn;
+#endif
     }
     store_jac28p(partials, seg, acc);
 }

@@ -14,6 +14,9 @@
 //     from LDS as k_accumulate reads its LDS-DMA stage -- but no random HBM gathers, no sorted
 //     index stream and no bucket boundaries.  Its time per contribution is the ceiling the
 //     accumulation could reach with a perfect memory system;
+//   * k_acc28p_ceiling: k_accumulate_r28p<G2>'s arithmetic (round 6: pair-sliced radix-2^28 Fq2,
+//     mbls_fq2_28.hpp) -- the same madd / mmadd over lane pairs, 16-point chunks, the same launch
+//     bounds, points from LDS;
 //   * k_ntt_ceiling: k_ntt_pass's round-5 radix-4 (2 x 2) DIT butterfly body (4 lazy FIPS Fr
 //     products, 8 add_2r / sub_2r) register-resident with twiddles from LDS, at the pass's launch
 //     bounds; k_ntt29_ceiling: the same body with the round-6 products (mbls_fr29.hpp: radix-2^29
@@ -30,6 +33,7 @@
 #include "mbls_fips.hpp"
 #include "mbls_fq28.hpp"
 #include "mbls_fr29.hpp"
+#include "mbls_fq2_28.hpp"
 
 #define CK(x)                                                                        \
     do {                                                                             \
@@ -196,6 +200,52 @@ __global__ __launch_bounds__(256, 3) void k_acc28_ceiling(const uint8_t* __restr
         r28::to_words(acc.y, out.y.v);
         r28::to_words(acc.z, out.z.v);
         store_jac<Fq>(partials, (size_t)tid * chunks_per_thread + ch, out);
+    }
+    clk_end(rec, c0, w0);
+}
+
+// G2 (round 6): pair-sliced radix-2^28 Fq2, lane j of a pair holding component j; the table holds
+// 64 G2 points (192 B: x0 x1 y0 y1), each lane reading its component's words
+#ifndef MBLS_ACC_G2_MINW
+#define MBLS_ACC_G2_MINW 2
+#endif
+template <int CHUNK>
+__global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_acc28p_ceiling(const uint8_t* __restrict__ table,
+                                                                          uint8_t* __restrict__ partials, Clk* rec,
+                                                                          uint32_t chunks_per_pair, uint32_t seed) {
+    unsigned long long c0, w0;
+    clk_begin(c0, w0);
+    __shared__ uint4 pts[PTS * 12];
+    for (int k = threadIdx.x; k < PTS * 12; k += blockDim.x) pts[k] = reinterpret_cast<const uint4*>(table)[k];
+    __syncthreads();
+    const uint32_t pair = (blockIdx.x * blockDim.x + threadIdx.x) >> 1, j = threadIdx.x & 1;
+    uint32_t h = seed ^ (pair * 0x9e3779b9u);  // pair-uniform stream
+    for (uint32_t ch = 0; ch < chunks_per_pair; ++ch) {
+        r28p::J28p acc = r28p::J28p::inf();
+        for (int e = 0; e < CHUNK; ++e) {
+            h = h * 1664525u + 1013904223u;
+            const uint32_t idx = (h >> 8) & (PTS - 1);
+            uint32_t xw[12], yw[12];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint4 xa = pts[idx * 12 + 3 * j + k], ya = pts[idx * 12 + 6 + 3 * j + k];
+                xw[4 * k] = xa.x, xw[4 * k + 1] = xa.y, xw[4 * k + 2] = xa.z, xw[4 * k + 3] = xa.w;
+                yw[4 * k] = ya.x, yw[4 * k + 1] = ya.y, yw[4 * k + 2] = ya.z, yw[4 * k + 3] = ya.w;
+            }
+            const r28::F28 qx = r28::unpack_shift8(xw);
+            r28::F28 qy = r28::unpack_shift8(yw);
+            if (h & 1) qy = r28::carry(r28::neg<r28::B512>(qy));
+            if (acc.is_inf()) {
+                acc = {r28::fold(qx), r28::fold(qy), r28p::one()};
+                continue;
+            }
+            bool done = false;
+            if (e == 1) done = r28p::mmadd(acc, qx, qy);
+            if (!done) done = r28p::madd(acc, qx, qy);
+            if (!done) acc = r28p::J28p::inf();  // (never for the random table)
+        }
+        Jacobian<PFq2> out{r28p::to_pf(acc.x), r28p::to_pf(acc.y), r28p::to_pf(acc.z)};
+        store_jac<PFq2>(partials, (size_t)pair * chunks_per_pair + ch, out);
     }
     clk_end(rec, c0, w0);
 }
@@ -405,6 +455,31 @@ int main(int argc, char** argv) {
                "\"contributions\": %.0f, \"ms\": %.4f, \"ns_per_contribution_chip\": %.6f, \"mhz_med\": %.0f, "
                "\"mhz_min\": %.0f, \"mhz_max\": %.0f, \"ms_per_2^20_g1_msm_contributions\": %.4f}",
                done, t28.ms, t28.ms * 1e6 / done, t28.mhz_med, t28.mhz_min, t28.mhz_max, t28.ms / done * 16777216.0);
+        // G2 pair-sliced: 2^(clog - 2) contributions (a G2 contribution costs ~3x a G1 one)
+        {
+            const size_t c2 = contributions / 4, chunks2 = c2 / 16;
+            const uint32_t pairs = threads / 2;
+            const uint32_t per2 = (uint32_t)((chunks2 + pairs - 1) / pairs);
+            std::vector<uint32_t> tab2(PTS * 48);
+            for (auto& w : tab2) w = (s = s * 1103515245u + 12345u);
+            for (int i = 0; i < PTS * 4; ++i) tab2[i * 12 + 11] &= 0x0fffffffu;  // < p
+            uint8_t *d_tab2, *d_part2;
+            CK(hipMalloc(&d_tab2, tab2.size() * 4));
+            CK(hipMemcpy(d_tab2, tab2.data(), tab2.size() * 4, hipMemcpyHostToDevice));
+            CK(hipMalloc(&d_part2, (size_t)pairs * per2 * 288));
+            auto LG2 = [&] {
+                hipLaunchKernelGGL(k_acc28p_ceiling<16>, dim3(threads / 256), dim3(256), 0, 0, d_tab2, d_part2, d_rec, per2, 77u);
+            };
+            Timing tg = run(LG2, d_rec, threads / 64, 5);
+            const double done2 = (double)pairs * per2 * 16;
+            // G2 2^20 MSM: psi split, 4n digit streams x 4 windows of c = 16
+            printf(",\n \"acc28p_ceiling\": {\"kernel\": \"k_acc28p_ceiling<16> (k_accumulate_r28p<G2> arithmetic: "
+                   "pair-sliced radix-2^28 Fq2; points from LDS)\", \"contributions\": %.0f, \"ms\": %.4f, "
+                   "\"ns_per_contribution_chip\": %.6f, \"mhz_med\": %.0f, \"ms_per_2^20_g2_msm_contributions\": %.4f}",
+                   done2, tg.ms, tg.ms * 1e6 / done2, tg.mhz_med, tg.ms / done2 * 16777216.0);
+            CK(hipFree(d_tab2));
+            CK(hipFree(d_part2));
+        }
         CK(hipFree(d_tab));
         CK(hipFree(d_part));
     }
