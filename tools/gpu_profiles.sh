@@ -18,7 +18,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_g2 -o run --outpu
   python3 $R/tools/stage_probe.py --group g2 --log 20 --reps 5 > $O/g2_stages.json 2> $O/g2_stages.err || exit 1
 i=0
 for P in "SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" \
-         "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+         "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
+         "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $P -d $O/pmc/p$i -o run --output-format csv -- \
     python3 $R/tools/pmc_probe.py --reps 3 > $O/pmc/probe_p$i.txt 2>&1 || { echo "pmc pass $i failed"; exit 1; }
@@ -41,5 +42,6 @@ import json, sys
 d = json.load(open(sys.argv[1]))["kernels"]
 for k in ("k_accumulate<G1>", "k_accumulate<G2>", "k_ntt_pass<true, false, false>", "k_ntt_pass<false, false, false>", "k_ntt_pass<false, true, false>"):
     r = d.get(k, {})
-    print(k, {c: r.get(c) for c in ("dispatches", "SQ_INSTS_VALU", "SQ_INSTS_VALU_INT64", "hbm_bytes_per_launch", "TCC_HIT_sum", "TCC_MISS_sum")})
+    print(k, {c: r.get(c) for c in ("dispatches", "SQ_INSTS_VALU", "SQ_INSTS_VALU_INT64", "hbm_bytes_per_launch", "TCC_HIT_sum", "TCC_MISS_sum",
+                                    "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES", "SQ_INSTS_LDS", "SQ_ACTIVE_INST_LDS")})
 PY

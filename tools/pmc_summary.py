@@ -18,7 +18,7 @@ import sys
 from collections import defaultdict
 
 # (substring, key): G1 / G2 instances of the templated MSM kernels kept apart
-ALIASES = (("k_accumulate_r28<mbls::Fp<mbls::FqCfg>", "k_accumulate<G1>"), ("k_accumulate<mbls::Fp<mbls::FqCfg>", "k_accumulate<G1>"), ("k_accumulate<mbls::Fq2", "k_accumulate<G2>"),
+ALIASES = (("k_accumulate_r28p<mbls::Fq2", "k_accumulate<G2>"), ("k_accumulate_r28<mbls::Fp<mbls::FqCfg>", "k_accumulate<G1>"), ("k_accumulate<mbls::Fp<mbls::FqCfg>", "k_accumulate<G1>"), ("k_accumulate<mbls::Fq2", "k_accumulate<G2>"),
            ("k_bucket_small<mbls::Fp<mbls::FqCfg>", "k_bucket_small<G1>"), ("k_bucket_small<mbls::Fq2", "k_bucket_small<G2>"))
 KEYS = ("k_accumulate", "k_ntt_pass<true, false, false>", "k_ntt_pass<false, false, false>",
         "k_ntt_pass<false, true, false>", "k_ntt_pass<false, true, true>", "k_scatter", "k_digits_tiled",
