@@ -16,7 +16,8 @@
 // giving x R 2^8 = x R' exactly with no arithmetic (< 256 p, normalised limbs), and `to_words`
 // divides by 2^8 (one 8-bit Montgomery step) and reduces to the canonical 32-bit words.
 //
-// Bounds (checked by tools/fq28_bench.hip against the FIPS path, bit-exact):
+// Bounds (at their maxima: tests/test_gpu_limbs.py, limb-exact model on the CPU and the device code
+// through tests/diag/limbs_diag.hip; random chains bit-exact against the FIPS path: tools/fq28_bench):
 //   * product inputs: limbs a_i < 2^A, b_j < 2^B with 14 * 2^(A+B) + 14 * 2^56 + carry < 2^64
 //     (A + B <= 60.1; the squaring doubles one operand: A + B + 1 <= 60.1 for 7 cross terms);
 //   * product outputs are normalised (limbs < 2^28) and < p (1 + a b / 2^392) for inputs a, b:
@@ -221,8 +222,12 @@ MBLS_DEV F28 carry(const F28& a) {
     return r;
 }
 
-// normalise and fold: limbs < 2^31, value < 2^391 -> normalised, congruent, < 3p.  q from the
-// top limb (plus the carry the limb below could add) under-estimates floor(v / p) by <= 2.
+// normalise and fold: limbs < 2^32 (no uint32 wrap; the sums work in int64), value < 2^391 ->
+// normalised, congruent, < 3p.  With t = l_13 + (l_12 >> 28) the value is below (t + 1 + 2^-23)
+// 2^364 (the rest of l_12 and every lower limb < 2^32 add < 2^364 + 2^341), and p >= P_13 2^364, so
+// v / p - q < (t + 1.001) / P_13 - t / (P_13 + 1) + 1 = t / (P_13 (P_13 + 1)) + 1.001 / P_13 + 1
+// < 1.02 for t < 2^27: q under-estimates floor(v / p) by <= 2 (mmadd's sub<B512>(y2, acc.y) with a
+// negated y2 reaches limbs ~2^31.3; pinned by tests/test_gpu_limbs.py at the limb maxima).
 MBLS_DEV F28 fold(const F28& a) {
     const uint32_t top = a.l[NL - 1] + (a.l[NL - 2] >> 28);
     const int32_t nq = -(int32_t)(uint32_t)(((uint64_t)top * FOLD_RECIP) >> 40);

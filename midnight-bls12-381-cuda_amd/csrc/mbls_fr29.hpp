@@ -17,7 +17,7 @@
 // twiddle tables hold w R' mod r (k_twiddles), so mul(x R, w R') = x w R: the products land in
 // the data's own Montgomery form with no conversion.
 //
-// Bounds (tests/test_gpu_fr29.py drives them at the extremes, bit-exact against Python integers):
+// Bounds (tests/test_gpu_limbs.py drives them at the extremes, bit-exact against Python integers):
 //   * column k: <= 9 products a_i b_j + <= 8 terms m_i r_j (< 2^58) + m_k (< 2^29) + the carry
 //     (< 2^35) < 2^64 needs 9 2^(A+B) < 2^64 - 2^61, i.e. A + B <= 60.6 for limbs a_i < 2^A,
 //     b_j < 2^B -- here both operands are normalised (A = B = 29);
