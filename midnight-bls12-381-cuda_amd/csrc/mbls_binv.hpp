@@ -164,6 +164,57 @@ MBLS_HD void lincomb_mod(uint32_t (&r)[N], const uint32_t (&u)[N], const uint32_
     for (int i = 0; i < N; ++i) r[i] = t[i];
 }
 
+// One of the four updates of an outer step, as one branch-free body for the four-lane form
+// (mbls_binv_quad.hpp: one role per lane of a DPP quad).  exact lanes (modl false): r = |f x + g y| / 2^K, neg = (f x + g y < 0, nonzero) -- lincomb_shift;
+// mod lanes (modl true): r = (f x + g y) / 2^K mod m -- lincomb_mod.  |f|, |g| <= 2^K.
+template <int N>
+MBLS_HD void lincomb_role(uint32_t (&r)[N], bool& neg_out, const uint32_t (&x)[N], const uint32_t (&y)[N], int64_t f,
+                          int64_t g, bool modl, const uint32_t (&m)[N], uint32_t ninv) {
+    uint32_t P[N + 1], Q[N + 1], S[N + 1];
+    mul_small<N>(P, x, (uint32_t)(f < 0 ? -f : f));
+    mul_small<N>(Q, y, (uint32_t)(g < 0 ? -g : g));
+    const bool neg = signed_sum<N + 1>(S, P, f < 0, Q, g < 0);
+    {  // mod lanes, negative: |S| <= 2^(K+1) m, S <- 2^(K+1) m - |S|
+        const bool fix = modl && neg;
+        int64_t br = 0;
+        for (int i = 0; i <= N; ++i) {
+            const uint32_t lo = i == 0 ? 0u : m[i - 1] >> (31 - K);
+            const uint32_t mw = (i < N ? m[i] << (K + 1) : 0u) | lo;
+            int64_t d = (int64_t)mw - S[i] + br;
+            br = d >> 32;
+            S[i] = fix ? (uint32_t)d : S[i];
+        }
+    }
+    // mod lanes: S + k m = 0 (mod 2^K); exact lanes: k = 0 (S is a multiple of 2^K already)
+    const uint32_t k = modl ? (S[0] * ninv) & ((1u << K) - 1) : 0u;
+    uint64_t c = 0;
+    for (int i = 0; i <= N; ++i) {
+        c += (uint64_t)S[i] + (i < N ? (uint64_t)m[i] * k : 0ull);
+        S[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    uint32_t t[N + 1];
+    for (int i = 0; i < N; ++i) t[i] = (S[i] >> K) | (S[i + 1] << (32 - K));
+    t[N] = S[N] >> K;
+    for (int q = 0; q < 2; ++q) {  // mod lanes: < 3m -> < m
+        uint32_t d[N + 1];
+        int64_t br = 0;
+        for (int i = 0; i <= N; ++i) {
+            int64_t xx = (int64_t)t[i] - (i < N ? m[i] : 0u) + br;
+            d[i] = (uint32_t)xx;
+            br = xx >> 32;
+        }
+        const bool keep = br || !modl;
+        for (int i = 0; i <= N; ++i) t[i] = keep ? t[i] : d[i];
+    }
+    uint32_t z = 0;
+    for (int i = 0; i < N; ++i) {
+        r[i] = t[i];
+        z |= t[i];
+    }
+    neg_out = neg && z != 0;
+}
+
 // out = 1 / y mod m (plain integers, y in [1, m), m odd, gcd(y, m) = 1).  Returns the number of
 // outer steps (<= 2 * bitlen(m) / K + 2 for valid input; capped so a bad input still ends).
 // The (u, v) update of outer step k is independent of the (a, b) work of step k + 1, so it runs
@@ -230,6 +281,74 @@ MBLS_HD int inverse(uint32_t (&out)[N], const uint32_t (&y)[N], const uint32_t (
     }
     uint32_t nv[N];
     lincomb_mod<N>(nv, u, v, pf1, pg1, m, ninv);  // the last step's update (only v is needed)
+    for (int i = 0; i < N; ++i) out[i] = nv[i];
+    return steps;
+}
+
+// The four-lane form (mbls_binv_quad.hpp::inverse_quad) with its four roles run one after the
+// other: the same outer loop, role selection and exchange, for the host check of lincomb_role
+// (tests/binv_host.cpp).  Returns the number of outer steps.
+template <int N>
+MBLS_HD int inverse_roles(uint32_t (&out)[N], const uint32_t (&y)[N], const uint32_t (&m)[N], uint32_t ninv) {
+    uint32_t a[N], b[N], u[N], v[N];
+    for (int i = 0; i < N; ++i) {
+        a[i] = y[i];
+        b[i] = m[i];
+        u[i] = i == 0 ? 1u : 0u;
+        v[i] = 0;
+    }
+    int64_t pf0 = (int64_t)1 << K, pg0 = 0, pf1 = 0, pg1 = (int64_t)1 << K;
+    int steps = 0;
+    const int cap = (64 * N) / K + 8;
+    while (!is_zero<N>(a) && steps < cap) {
+        ++steps;
+        const int nl = bitlen_or<N>(a, b);
+        const int n = nl > 64 ? nl : 64;
+        uint64_t xa = (a[0] & 0x7fffffffu) | (top33<N>(a, n - 33) << 31);
+        uint64_t xb = (b[0] & 0x7fffffffu) | (top33<N>(b, n - 33) << 31);
+        uint64_t F0 = 1, F1 = 1ull << 32;
+        for (int j = 0; j < K; ++j) {
+            const bool odd = (xa & 1) != 0;
+            const bool lt = xa < xb;
+            const bool sw = odd && lt;
+            const uint64_t d = lt ? xb - xa : xa - xb;
+            const uint64_t G0 = sw ? F1 : F0, G1 = sw ? F0 : F1;
+            xb = sw ? xa : xb;
+            xa = (odd ? d : xa) >> 1;
+            F0 = odd ? G0 - G1 : G0;
+            F1 = G1 << 1;
+        }
+        int64_t f0 = (int32_t)(uint32_t)F0, g0 = ((int64_t)F0 - f0) >> 32;
+        int64_t f1 = (int32_t)(uint32_t)F1, g1 = ((int64_t)F1 - f1) >> 32;
+        uint32_t R[4][N];
+        bool neg[4];
+        for (int role = 0; role < 4; ++role) {
+            const bool modl = role >= 2;
+            const int64_t f = role == 0 ? f0 : role == 1 ? f1 : role == 2 ? pf0 : pf1;
+            const int64_t g = role == 0 ? g0 : role == 1 ? g1 : role == 2 ? pg0 : pg1;
+            lincomb_role<N>(R[role], neg[role], modl ? u : a, modl ? v : b, f, g, modl, m, ninv);
+        }
+        for (int i = 0; i < N; ++i) {
+            a[i] = R[0][i];
+            b[i] = R[1][i];
+            u[i] = R[2][i];
+            v[i] = R[3][i];
+        }
+        if (neg[0]) {
+            f0 = -f0;
+            g0 = -g0;
+        }
+        if (neg[1]) {
+            f1 = -f1;
+            g1 = -g1;
+        }
+        pf0 = f0;
+        pg0 = g0;
+        pf1 = f1;
+        pg1 = g1;
+    }
+    uint32_t nv[N];
+    lincomb_mod<N>(nv, u, v, pf1, pg1, m, ninv);
     for (int i = 0; i < N; ++i) out[i] = nv[i];
     return steps;
 }

@@ -229,6 +229,7 @@ MBLS_DEV Fp<C> mul_cios(const Fp<C>& a, const Fp<C>& b) {
 }  // namespace mbls
 #include "mbls_fips.hpp"
 #include "mbls_binv.hpp"
+#include "mbls_binv_quad.hpp"
 namespace mbls {
 
 template <class C>
@@ -394,6 +395,27 @@ MBLS_DEV Fq2 operator*(const Fq2& a, const Fq2& b) { return fq2_mul(a, b); }
 MBLS_DEV Fq2 sqr(const Fq2& a) { return fq2_sqr(a); }
 MBLS_DEV Fq2 inv(const Fq2& a) {
     Fq n = inv(sqr(a.c0) + sqr(a.c1));
+    return {a.c0 * n, neg(a.c1 * n)};
+}
+
+// inv() on the four lanes of a DPP quad (all active, same input; mbls_binv_quad.hpp): the outer
+// step's four 12-word updates run one per lane instead of one after the other
+template <class C>
+MBLS_DEV Fp<C> inv_quad(const Fp<C>& a_in) {
+    constexpr int N = C::N;
+    Fp<C> a = a_in;
+    reduce_once(a);
+    if (a.is_zero()) return a;
+    uint32_t m[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) m[i] = C::MOD[i];
+    Fp<C> x;
+    binv::inverse_quad<N>(x.v, a.v, m, C::NINV);
+    const Fp<C> r2 = Fp<C>::r2();
+    return x * (r2 * r2);
+}
+MBLS_DEV Fq2 inv_quad(const Fq2& a) {
+    Fq n = inv_quad(sqr(a.c0) + sqr(a.c1));
     return {a.c0 * n, neg(a.c1 * n)};
 }
 

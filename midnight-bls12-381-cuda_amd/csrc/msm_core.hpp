@@ -1171,6 +1171,9 @@ __global__ __launch_bounds__(256) void k_reduce_tree4(const uint8_t* __restrict_
     }
 }
 
+#ifndef MBLS_FINAL_QUAD
+#define MBLS_FINAL_QUAD 1  // k_final_icicle's inversion on a lane quad (icicle_point_quad)
+#endif
 // final fold over window groups: sum_w 2^(c w) G_w  (one chain)
 template <class F, int MODE>
 MBLS_DEV auto final_fold(const uint8_t* __restrict__ windows, int Wg, int c) {
@@ -1261,6 +1264,25 @@ MBLS_DEV void icicle_point(const Jacobian<F>& p, uint8_t* out, size_t i) {
     store_jac<F>(out, i, o);
 }
 
+// icicle_point on the four lanes of a DPP quad (all active, same p): the inversion runs as
+// inv_quad (mbls_binv_quad.hpp); lane 0 of the quad stores
+template <class F>
+MBLS_DEV void icicle_point_quad(const Jacobian<F>& p, uint8_t* out, size_t i) {
+    Jacobian<F> o;
+    if (p.is_inf()) {
+        o.x = F::zero();
+        o.y = one_std<F>();
+        o.z = F::zero();
+    } else {
+        const F zi = inv_quad(p.z);
+        const F zi2 = sqr(zi);
+        o.x = from_mont_f(p.x * zi2);
+        o.y = from_mont_f(p.y * zi2 * zi);
+        o.z = one_std<F>();
+    }
+    if ((__lane_id() & 3u) == 0) store_jac<F>(out, i, o);
+}
+
 // in and out may alias (in place)
 template <class F>
 __global__ __launch_bounds__(64) void k_jac_to_icicle(const uint8_t* in, uint8_t* out, int count) {
@@ -1296,7 +1318,11 @@ __global__ __launch_bounds__(64) void k_final_icicle(const uint8_t* __restrict__
 #if MBLS_HEAVY_TRACE
     const uint64_t t1 = wall_clock64();
 #endif
+#if MBLS_FINAL_QUAD
+    if (threadIdx.x < 4) icicle_point_quad<F>(p, out, 0);
+#else
     if (threadIdx.x == 0) icicle_point<F>(p, out, 0);
+#endif
 #if MBLS_HEAVY_TRACE
     if (threadIdx.x == 0) printf("FIN fold=%llu inv=%llu\n", t1 - t0, wall_clock64() - t1);
 #endif

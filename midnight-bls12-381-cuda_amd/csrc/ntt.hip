@@ -203,10 +203,12 @@ MBLS_DEV r29::F29 ldtw(const uint4* a, const uint4* b, const uint32_t* c, uint32
 // One pass of up to NTT_TILE_LOG DIT stages.
 //   FIRST: stages 1..L with the bit-reversal gather from `in`; else stages s0+1..s0+L in place.
 //   LAST:  store canonical values; SCALE (inverse, implies LAST): multiply them by n^-1.
-// One tile per workgroup, grid = tiles.  (Persistent workgroups walking several tiles were
-// measured 11% SLOWER, round 6: on gfx9 vmcnt counts loads and stores in one in-order counter, so
-// the first wait on the next tile's loads -- or on a twiddle load -- also waits for this tile's
-// stores, while a fresh workgroup starts with no stores outstanding; profiles/r06/README.md.)
+// One tile per workgroup, grid = tiles.  Persistent workgroups walking several tiles lost in every
+// form measured in round 6 (profiles/r06/README.md): reload after the stores (11% slower: vmcnt
+// counts loads and stores in one in-order counter, so the next tile's first wait also waits for
+// this tile's stores), the next tile prefetched into 32 VGPRs during the stage pairs (spills at 4
+// workgroups per CU, occupancy at 3: +6-11%), and the next tile LDS-DMA'd behind this tile's
+// stores (+7-13%), although a no-store pricing variant shows the stores at ~13% of the pass.
 // Index arithmetic is 32-bit (element indices inside a polynomial and the twiddle tables stay
 // below 2^31 for transforms <= 2^30), the tile is a uint4 LDS array (every access one b128),
 // and the 2r constants are literals (the pass is VALU-issue bound, profiles/r05/ntt_diag.txt).

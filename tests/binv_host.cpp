@@ -1,6 +1,6 @@
 // Host harness for csrc/mbls_binv.hpp (the device inversion's algorithm, compiled here with g++):
 // reads lines "<words> <hex word 0> ... <hex word words-1>" (12 = Fq modulus p, 8 = Fr modulus r),
-// prints "<outer steps> <inverse words...>".  Driven by tests/test_oracle.py::test_binary_gcd_inverse.
+// prints "<outer steps> <1 if the four-lane form (inverse_roles) agrees> <inverse words...>".  Driven by tests/test_oracle.py::test_binary_gcd_inverse.
 #include <cstdio>
 #include <cstdlib>
 
@@ -16,7 +16,11 @@ static void run(char* s, const uint32_t (&m)[N], uint32_t ninv) {
     uint32_t y[N], o[N];
     for (int i = 0; i < N; ++i) y[i] = (uint32_t)strtoul(s, &s, 16);
     const int steps = mbls::binv::inverse<N>(o, y, m, ninv);
-    printf("%d", steps);
+    uint32_t q[N];
+    const int qsteps = mbls::binv::inverse_roles<N>(q, y, m, ninv);  // the four-lane form, roles in turn
+    bool same = qsteps == steps;
+    for (int i = 0; i < N; ++i) same = same && q[i] == o[i];
+    printf("%d %d", steps, same ? 1 : 0);
     for (int i = 0; i < N; ++i) printf(" %08x", o[i]);
     printf("\n");
 }
