@@ -49,6 +49,9 @@ namespace mbls {
 #ifndef MBLS_NTT_THREADS
 #define MBLS_NTT_THREADS 256
 #endif
+#ifndef MBLS_NTT_DIRECT
+#define MBLS_NTT_DIRECT 1  // the pass's last stage group stores straight from registers (k_ntt_pass)
+#endif
 #ifndef MBLS_NTT_XCD
 #define MBLS_NTT_XCD 0  // 1: tiles of adjacent columns on the same XCD (shared L2 lines)
 #endif
@@ -268,8 +271,17 @@ __global__ __launch_bounds__(NTT_THREADS, 5) void k_ntt_pass(uint8_t* __restrict
         // ---- L DIT stages: pairs of stages as radix-4 (2 x 2) butterflies in registers (one LDS
         // round trip and one barrier per pair), an odd last stage as radix-2
         const uint32_t lo_base = FIRST ? 0u : g.lo0;
+        uint4* o = out + 2 * g.poly;
+        // the last stage group (MBLS_NTT_DIRECT) stores its outputs straight to HBM from registers:
+        // no LDS round trip, barrier or separate store loop; (row, c) of the tile -> its position
+        auto put = [&](uint32_t row, uint32_t c, Fr v) {
+            if (SCALE) v = v * scale;  // v < 2r, scale < r: the reduced product is canonical
+            else if (LAST) reduce_once(v);
+            st2(o, FIRST ? (bitrev(g.lo0 + c, colbits) << L) + row : g.hi_base + (row << s0) + g.lo0 + c, v);
+        };
         int l = 1;
         for (; l + 1 <= L; l += 2) {
+            const bool fin = MBLS_NTT_DIRECT && l + 2 > L;  // the last pair, no radix-2 stage after it
             const uint32_t h = 1u << (l - 1);  // stage l pairs rows (t, t + h), stage l + 1 rows (t, t + 2h)
             const int s = s0 + l;              // global stage of the first of the pair
             const uint32_t t1 = (1u << (s - 1)) - 1, t2 = (1u << s) - 1;  // stage tables s, s + 1
@@ -302,11 +314,19 @@ __global__ __launch_bounds__(NTT_THREADS, 5) void k_ntt_pass(uint8_t* __restrict
                 // stage l + 1: (y0, y2) with w_(2^(s+1))^j, (y1, y3) with w_(2^(s+1))^(j + h)
                 if (!triv) y2 = r29::mul_words(y2, w2);
                 y3 = r29::mul_words(y3, w3);
-                st2(lds, e0, add_2r(y0, y2));
-                st2(lds, e0 + 2 * stride, sub_2r(y0, y2));
-                st2(lds, e0 + stride, add_2r(y1, y3));
-                st2(lds, e0 + 3 * stride, sub_2r(y1, y3));
+                if (fin) {
+                    put(q, c, add_2r(y0, y2));
+                    put(q + 2 * h, c, sub_2r(y0, y2));
+                    put(q + h, c, add_2r(y1, y3));
+                    put(q + 3 * h, c, sub_2r(y1, y3));
+                } else {
+                    st2(lds, e0, add_2r(y0, y2));
+                    st2(lds, e0 + 2 * stride, sub_2r(y0, y2));
+                    st2(lds, e0 + stride, add_2r(y1, y3));
+                    st2(lds, e0 + 3 * stride, sub_2r(y1, y3));
+                }
             }
+            if (fin) return;
             if (MBLS_NTT_EXP != 2) __syncthreads();
         }
         if (l == L) {  // odd stage count: one radix-2 stage
@@ -324,14 +344,19 @@ __global__ __launch_bounds__(NTT_THREADS, 5) void k_ntt_pass(uint8_t* __restrict
                 const Fr a = ld2(lds, t0 * C + c);
                 Fr b = ld2(lds, t1 * C + c);
                 if (l > 1 || !FIRST) b = r29::mul_words(b, w);
-                st2(lds, t0 * C + c, add_2r(a, b));
-                st2(lds, t1 * C + c, sub_2r(a, b));
+                if (MBLS_NTT_DIRECT) {
+                    put(t0, c, add_2r(a, b));
+                    put(t1, c, sub_2r(a, b));
+                } else {
+                    st2(lds, t0 * C + c, add_2r(a, b));
+                    st2(lds, t1 * C + c, sub_2r(a, b));
+                }
             }
+            if (MBLS_NTT_DIRECT) return;
             __syncthreads();
         }
 
-        // ---- store
-        uint4* o = out + 2 * g.poly;
+        // ---- store (L = 0 only, or MBLS_NTT_DIRECT = 0)
         for (uint32_t e = threadIdx.x; e < T; e += NTT_THREADS) {
             Fr v;
             uint32_t dst;
