@@ -441,5 +441,130 @@ MBLS_DEV bool mmadd(J28& acc, const F28& x2_, const F28& y2_) {
     return true;
 }
 
+// ------------------------------------------------------------------------- XYZZ (round 6)
+// Extended Jacobian "XYZZ" coordinates: x = X / ZZ, y = Y / ZZZ with ZZ^3 = ZZZ^2 (ZZ = Z^2,
+// ZZZ = Z^3 for a Z that is never formed).  The accumulation's mixed addition (madd-2008-s) is
+// 6M + 2S + one lazy mul2 against madd-2007-bl's 6M + 3S + mul2 -- one squaring (~370 of ~4700
+// instructions) fewer per contribution -- and the full addition (add-2008-s) 10M + 2S + mul2
+// against add-2007-bl's 10M + 4S + mul2.  The chunk's second point (mmadd: ZZ = PP, ZZZ = PPP) costs
+// the same as the Jacobian one.  Partials leave the accumulation in XYZZ words (4 x 48 B); the
+// bucket sums add them in XYZZ and convert each bucket sum once (x_to_jac) for the reduction.
+// Invariant between steps: x, y folded (normalised, < 3p); zz, zzz normalised (< 3p).  The limb
+// bounds of every step are restated in tests/limbs_model.py (_fq28_formulas) and pinned at their
+// extremes by tests/test_gpu_limbs.py; largest column: mul2's R (carried) x (Q - X3 against B16)
+// plus neg<B16>(y) x PPP, < 2^62.4.
+struct X28 {
+    F28 x, y, zz, zzz;
+    MBLS_DEV bool is_inf() const {
+        uint32_t t = 0;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) t |= zz.l[i];
+        return t == 0;  // infinity is exactly zz = 0 (set, never computed)
+    }
+    MBLS_DEV static X28 inf() { return {F28::one(), F28::one(), F28::zero(), F28::zero()}; }
+};
+
+// dbl-2008-s-1 (a = 0; exceptional path only: P == Q inside a bucket)
+MBLS_DEV void xdbl(X28& a) {
+    const F28 U = x2(a.y);  // limbs < 2^29
+    const F28 V = sqr(U);
+    const F28 W = mul(U, V);
+    const F28 S = mul(a.x, V);
+    const F28 A = sqr(a.x);
+    const F28 M = add(x2(A), A);  // 3 X^2: limbs < 3 2^28
+    const F28 X3 = fold(sub<B32>(sqr(M), x2(S)));
+    a.y = mul2(M, sub<B16>(S, X3), neg<B16>(a.y), W);
+    a.x = X3;
+    a.zz = mul(V, a.zz);
+    a.zzz = mul(W, a.zzz);
+}
+
+// acc + q, q = (x2, y2) affine from unpack_shift8 (< 256 p, normalised; y2 may be neg<B512> of one:
+// < 512 p, limbs < 2^30.4), not the identity: madd-2008-s with the lazy Y3.  Park: as madd.
+template <class Park>
+MBLS_DEV void xmadd(X28& acc, const F28& x2_, const F28& y2_, Park& pk) {
+    if (acc.is_inf()) {
+        acc = {fold(x2_), fold(y2_), F28::one(), F28::one()};
+        return;
+    }
+    const F28 U2 = mul(x2_, acc.zz);
+    const F28 S2 = mul(y2_, acc.zzz);
+    const F28 Pd = sub<B16>(U2, acc.x);          // limbs < 2^29.6
+    const F28 R = carry(sub<B16>(S2, acc.y));    // normalised but the top limb
+    pk.put(1, acc.y);
+    const F28 PP = sqr(Pd);
+    if (is_zero_lt2p(PP)) {  // U2 == X mod p: equal or opposite points
+        acc.y = pk.get(1);
+        if (is_zero_mod(R))
+            xdbl(acc);
+        else
+            acc = X28::inf();
+        return;
+    }
+    // ordered for register pressure: zz dies at ZZ3, P at PPP, zzz at ZZZ3, x and PP at Q
+    acc.zz = mul(acc.zz, PP);
+    const F28 PPP = mul(Pd, PP);
+    acc.zzz = mul(acc.zzz, PPP);
+    const F28 Q = mul(acc.x, PP);
+    acc.x = fold(sub<B32>(sub<B16>(sqr(R), PPP), x2(Q)));
+    acc.y = mul2(R, sub<B16>(Q, acc.x), neg<B16>(pk.get(1)), PPP);
+}
+MBLS_DEV void xmadd(X28& acc, const F28& x2_, const F28& y2_) {
+    ParkReg pk;
+    xmadd(acc, x2_, y2_, pk);
+}
+
+// acc fresh from the chunk's first point (zz = zzz = R'-one, x, y folded) + q: ZZ = PP, ZZZ = PPP.
+// Returns false (acc untouched) when x1 == x2 mod p, left to xmadd's branches.
+MBLS_DEV bool xmmadd(X28& acc, const F28& x2_, const F28& y2_) {
+    const F28 Pd = fold(sub<B512>(x2_, acc.x));
+    const F28 PP = sqr(Pd);
+    if (is_zero_lt2p(PP)) return false;
+    const F28 R = fold(sub<B512>(y2_, acc.y));  // limbs < 2^31.4 before the fold
+    const F28 PPP = mul(Pd, PP);
+    const F28 Q = mul(acc.x, PP);
+    const F28 X3 = fold(sub<B32>(sub<B16>(sqr(R), PPP), x2(Q)));
+    acc.y = mul2(R, sub<B16>(Q, X3), neg<B16>(acc.y), PPP);
+    acc.x = X3;
+    acc.zz = PP;
+    acc.zzz = PPP;
+    return true;
+}
+
+// acc + a partial (x2, y2, zz2, zzz2), each from unpack_shift8 (< 256 p, normalised), zz2 != 0:
+// add-2008-s with the lazy Y3
+MBLS_DEV void xadd(X28& acc, const F28& x2_, const F28& y2_, const F28& zz2, const F28& zzz2) {
+    if (acc.is_inf()) {
+        acc = {fold(x2_), fold(y2_), fold(zz2), fold(zzz2)};
+        return;
+    }
+    const F28 U1 = mul(acc.x, zz2);
+    const F28 U2 = mul(x2_, acc.zz);
+    const F28 S1 = mul(acc.y, zzz2);
+    const F28 S2 = mul(y2_, acc.zzz);
+    const F28 Pd = sub<B16>(U2, U1);
+    const F28 R = carry(sub<B16>(S2, S1));
+    const F28 PP = sqr(Pd);
+    if (is_zero_lt2p(PP)) {  // equal or opposite points
+        if (is_zero_mod(R))
+            xdbl(acc);
+        else
+            acc = X28::inf();
+        return;
+    }
+    const F28 PPP = mul(Pd, PP);
+    const F28 Q = mul(U1, PP);
+    acc.zz = mul(mul(acc.zz, zz2), PP);
+    acc.zzz = mul(mul(acc.zzz, zzz2), PPP);
+    acc.x = fold(sub<B32>(sub<B16>(sqr(R), PPP), x2(Q)));
+    acc.y = mul2(R, sub<B16>(Q, acc.x), neg<B16>(S1), PPP);
+}
+
+// XYZZ -> Jacobian with Z = ZZZ: (X ZZ^2, Y ZZZ^2, ZZZ) (x = X ZZ^2 / ZZ^3, y = Y ZZZ^2 / ZZZ^3)
+MBLS_DEV J28 x_to_jac(const X28& a) {
+    if (a.is_inf()) return J28::inf();
+    return {mul(a.x, sqr(a.zz)), mul(a.y, sqr(a.zzz)), a.zzz};
+}
+
 }  // namespace r28
 }  // namespace mbls

@@ -318,6 +318,36 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
 #ifndef MBLS_BS_R28
 #define MBLS_BS_R28 1  // light bucket sums (k_bucket_small, G1) in radix 2^28 too
 #endif
+#ifndef MBLS_ACC_XYZZ
+#define MBLS_ACC_XYZZ 1  // G1 accumulation and light / slice-chain bucket sums in XYZZ (r28::X28)
+#endif
+// a chunk partial's bytes: G1 partials are XYZZ words (x, y, zz, zzz) when the accumulation runs in
+// XYZZ, Jacobian otherwise
+template <class F>
+struct PartialBytes {
+    static constexpr size_t value = 3 * sizeof(F);  // Jacobian
+};
+template <>
+struct PartialBytes<Fq> {
+    static constexpr size_t value = (MBLS_ACC_XYZZ && MBLS_ACC_R28 && MBLS_ACC_LDS && MBLS_BS_R28) ? 192 : 144;
+};
+static_assert(!MBLS_ACC_XYZZ || (MBLS_ACC_R28 && MBLS_ACC_LDS && MBLS_BS_R28),
+              "XYZZ partials need the radix-2^28 accumulation and bucket sums");
+MBLS_DEV void store_xyzz28(uint8_t* __restrict__ partials, uint32_t seg, const r28::X28& acc) {
+    uint4* q = reinterpret_cast<uint4*>(partials + (size_t)seg * 192);
+    const bool inf = acc.is_inf();
+    auto put = [&](int k, const r28::F28& c) {
+        uint32_t w[12];
+        r28::to_words(c, w);
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            q[3 * k + j] = inf ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+    };
+    put(0, acc.x);
+    put(1, acc.y);
+    put(2, acc.zz);
+    put(3, acc.zzz);
+}
 MBLS_DEV void store_jac28(uint8_t* __restrict__ partials, uint32_t seg, const r28::J28& acc) {
     Jacobian<Fq> out;
     if (acc.is_inf()) {
@@ -354,7 +384,19 @@ __global__ __launch_bounds__(256, MBLS_ACC_R28_MINW) void k_accumulate_r28(const
     while (offsets[b + 1] <= beg) ++b;
     uint32_t seg = chunk_off[b] + (t - offsets[b] / chunk);
     uint32_t bend = offsets[b + 1];
-    r28::J28 acc = r28::J28::inf();
+#if MBLS_ACC_XYZZ
+    using Acc = r28::X28;
+#else
+    using Acc = r28::J28;
+#endif
+    Acc acc = Acc::inf();
+    auto flush = [&](uint32_t sg) __attribute__((always_inline)) {
+#if MBLS_ACC_XYZZ
+        store_xyzz28(partials, sg, acc);
+#else
+        store_jac28(partials, sg, acc);
+#endif
+    };
     __shared__ uint4 stage[2][256 / 64][6][64];
 #if MBLS_ACC_R28_PARK
     // acc.y parked in the lane's half of the stage that the current point was just read from
@@ -419,8 +461,8 @@ __global__ __launch_bounds__(256, MBLS_ACC_R28_MINW) void k_accumulate_r28(const
         if (e + 1 < end) issue(vn, slot ^ 1u);  // the other slot was read one addition ago
         const uint32_t vnn = e + 2 < end ? sorted[e + 2] : vn;
         if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
-            store_jac28(partials, seg, acc);
-            acc = r28::J28::inf();
+            flush(seg);
+            acc = Acc::inf();
             do {
                 ++b;
             } while (offsets[b + 1] == e);
@@ -432,18 +474,23 @@ __global__ __launch_bounds__(256, MBLS_ACC_R28_MINW) void k_accumulate_r28(const
             r28::F28 qy = r28::unpack_shift8(yw);
             if (v & 1) qy = r28::neg<r28::B512>(qy);  // -P: < 512 p, limbs < 2^30.4 (mbls_fq28.hpp)
             bool done = false;
-            if (MBLS_ACC_MMADD && e == beg + 1 && !acc.is_inf()) done = r28::mmadd(acc, qx, qy);
 #if MBLS_ACC_R28_PARK
             ParkStage pk{&stage[slot][wv][0][ln]};
 #else
             r28::ParkReg pk;
 #endif
+#if MBLS_ACC_XYZZ
+            if (MBLS_ACC_MMADD && e == beg + 1 && !acc.is_inf()) done = r28::xmmadd(acc, qx, qy);
+            if (!done) r28::xmadd(acc, qx, qy, pk);
+#else
+            if (MBLS_ACC_MMADD && e == beg + 1 && !acc.is_inf()) done = r28::mmadd(acc, qx, qy);
             if (!done) r28::madd(acc, qx, qy, pk);
+#endif
         }
         v = vn;
         vn = vnn;
     }
-    store_jac28(partials, seg, acc);
+    flush(seg);
 }
 
 // ------------------------------------------------------------------------------------
@@ -747,7 +794,25 @@ MBLS_DEV bool load_j28(const uint8_t* __restrict__ base, size_t i, r28::F28& x, 
     z = r28::unpack_shift8(w[2]);
     return true;
 }
-// r28 lane addition of chunk partial k (G1: the light path's and the slice chains' form)
+// r28 XYZZ addition of chunk partial k (G1 with MBLS_ACC_XYZZ: the light path's and the slice
+// chains' form); the identity (zz = 0) adds nothing
+MBLS_DEV void r28_add_partial(r28::X28& acc, const uint8_t* __restrict__ partials, uint32_t k) {
+    const uint4* q = reinterpret_cast<const uint4*>(partials + (size_t)k * 192);
+    uint32_t w[4][12], zany = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint4 u = q[3 * c + j];
+            w[c][4 * j] = u.x, w[c][4 * j + 1] = u.y, w[c][4 * j + 2] = u.z, w[c][4 * j + 3] = u.w;
+        }
+#pragma unroll
+    for (int j = 0; j < 12; ++j) zany |= w[2][j];
+    if (zany)
+        r28::xadd(acc, r28::unpack_shift8(w[0]), r28::unpack_shift8(w[1]), r28::unpack_shift8(w[2]),
+                  r28::unpack_shift8(w[3]));
+}
+// r28 lane addition of Jacobian chunk partial k (G1 without MBLS_ACC_XYZZ)
 MBLS_DEV void r28_add_partial(r28::J28& acc, const uint8_t* __restrict__ partials, uint32_t k) {
     const uint4* q = reinterpret_cast<const uint4*>(partials + (size_t)k * 144);
     uint32_t w[3][12], zany = 0;
@@ -860,8 +925,14 @@ MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t
         // the rows
         uint32_t live = min(CHAINS, c1 - c0);
         if constexpr (std::is_same<L, Fq>::value && MBLS_BS_R28) {
+#if MBLS_ACC_XYZZ
+            r28::X28 xacc = r28::X28::inf();
+            for (uint32_t k = c0 + j; k < c1; k += CHAINS) r28_add_partial(xacc, partials, k);
+            r28::J28 acc = r28::x_to_jac(xacc);  // the lane tree below adds Jacobian chain sums
+#else
             r28::J28 acc = r28::J28::inf();
             for (uint32_t k = c0 + j; k < c1; k += CHAINS) r28_add_partial(acc, partials, k);
+#endif
             store_jac28(sh, j, acc);
             __syncthreads();
             for (; live > 16; live = (live + 1) / 2) {
@@ -980,10 +1051,17 @@ __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32
     const uint32_t b = perm[t];
     const uint32_t k0 = chunk_off[b], k1 = chunk_off[b + 1];
     if constexpr (std::is_same<L, Fq>::value && MBLS_BS_R28) {
-        // radix 2^28 (mbls_fq28.hpp jadd; same values as jac_add, round 5)
+        // radix 2^28: XYZZ sums of XYZZ partials (add-2008-s), one conversion per bucket (round 6);
+        // Jacobian jadd otherwise (round 5)
+#if MBLS_ACC_XYZZ
+        r28::X28 acc = r28::X28::inf();
+        for (uint32_t k = k0; k < k1; ++k) r28_add_partial(acc, partials, k);
+        store_jac28(buckets, b, r28::x_to_jac(acc));
+#else
         r28::J28 acc = r28::J28::inf();
         for (uint32_t k = k0; k < k1; ++k) r28_add_partial(acc, partials, k);
         store_jac28(buckets, b, acc);
+#endif
         return;
     }
     Jacobian<L> acc = Jacobian<L>::inf();
@@ -1434,7 +1512,7 @@ struct MsmScratchSizes {
 #endif
 inline uint32_t wave_min_chains(bool fq2 = false) { return fq2 ? MBLS_WAVE_MIN_G2 : MBLS_WAVE_MIN; }
 
-inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks) {
+inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks, size_t part) {
     MsmScratchSizes z;
     // the per-call image table; with bstride > 1 also the compact copy of the points (2n rows)
     z.phi = P.split > 1 && !P.prepared ? align_up(P.pts / P.split * (P.split - 1 + (P.bstride > 1 ? 1 : 0)) * aff) : 0;
@@ -1473,7 +1551,7 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
                      4);
     z.owner = align_up((size_t)max_chunks * 4);
     z.first = align_up((NC / P.chunk + 2) * 4);
-    z.partials = align_up((size_t)max_chunks * jac);
+    z.partials = align_up((size_t)max_chunks * part);  // part: a chunk partial's bytes (PartialBytes)
     z.buckets = align_up((size_t)P.TB * jac);
     // V / U ping-pong halves sized for the widest level's outputs (k_reduce_scaled)
     const size_t mo0 = P.levels ? (P.level_m[0] + P.seg(0) - 1) / P.seg(0) : 1;
@@ -1608,7 +1686,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     const uint32_t TB = P.TB;
     const size_t NC = P.contributions;
     const uint32_t max_chunks = (uint32_t)(NC / P.chunk + TB + 1);
-    MsmScratchSizes z = msm_scratch_sizes(P, JAC, AFF, max_chunks);
+    MsmScratchSizes z = msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value);
     uint32_t* keys = (uint32_t*)arena.take(z.keys);
     uint32_t* vals = (uint32_t*)arena.take(z.vals);
     uint32_t* ranks = (uint32_t*)arena.take(z.ranks);
@@ -1855,7 +1933,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
         fprintf(stderr, "[mbls] msm n=%d c=%d W=%d Wg=%d split=%d TB=%u contributions=%zu chunk=%u levels=%d\n", msm_size,
                 P.c, P.W, P.Wg, P.split, P.TB, P.contributions, P.chunk, P.levels);
     uint32_t max_chunks = (uint32_t)(P.contributions / P.chunk + P.TB + 1);
-    size_t scratch = msm_scratch_sizes(P, JAC, AFF, max_chunks).total();
+    size_t scratch = msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value).total();
     const bool piped = batch > 1 && batch_pipe() > 0;
     er = lease.reserve(st_s + st_b + st_r + scratch * (piped ? 2 : 1) + 4096);
     if (er != MBLS_SUCCESS) return er;

@@ -15,8 +15,8 @@
 
 using namespace mbls;
 
-static constexpr int IN_W = 5 * 16;  // words per case: 5 operands of up to 16 words
-static constexpr int OUT_W = 48;     // words per case
+static constexpr int IN_W = 8 * 16;  // words per case: 8 operands of up to 16 words
+static constexpr int OUT_W = 64;     // words per case
 
 MBLS_DEV r28::F28 f28(const uint32_t* p) {
     r28::F28 r;
@@ -39,6 +39,9 @@ MBLS_DEV r29::F29 f29(const uint32_t* p) {
 //   r28:  0 mul(x0, x1)   1 sqr(x0)   2 mul2(x0, x1, x2, x3)   3 fold(x0)   4 to_words(x0) (12 words)
 //         5 carry(x0)   6 is_zero_mod(x0) (1 word)   7 madd(acc = x0, x1, x2; q = x3, x4): 42 words
 //         8 mmadd(acc = x0, x1, one; q = x3, x4): 42 words + the flag
+//   XYZZ: 9 xmadd(acc = x0..x3; q = x4, x5): 56 words   10 xmmadd(acc = x0, x1, one, one; q = x4, x5):
+//         56 words + the flag   11 xadd(acc = x0..x3; partial x4..x7)   12 xdbl(x0..x3)
+//         13 x_to_jac(x0..x3): 42 words
 //  r29: 20 mul(x0, x1)   21 unpack(words x0)   22 pack(x0) (8 words)   23 mul_words(words x0, x1)
 //  pair-sliced Fq2 (mbls_fq2_28.hpp): rows 2i, 2i + 1 are the two lanes of case i (component 0, 1):
 //       30 madd(acc = x0, x1, x2; q = x3, x4): 42 words + the flag   31 mmadd(acc = x0, x1; q = x3, x4)
@@ -75,6 +78,32 @@ __global__ void k_limbs(int op, const uint32_t* __restrict__ in, uint32_t* __res
             put28(o + 14, acc.y);
             put28(o + 28, acc.z);
             o[42] = done ? 1u : 0u;
+            break;
+        }
+        case 9:
+        case 10:
+        case 11:
+        case 12:
+        case 13: {
+            r28::X28 acc{f28(x), f28(x + 16), op == 10 ? r28::F28::one() : f28(x + 32),
+                         op == 10 ? r28::F28::one() : f28(x + 48)};
+            bool done = true;
+            if (op == 9) r28::xmadd(acc, f28(x + 64), f28(x + 80));
+            if (op == 10) done = r28::xmmadd(acc, f28(x + 64), f28(x + 80));
+            if (op == 11) r28::xadd(acc, f28(x + 64), f28(x + 80), f28(x + 96), f28(x + 112));
+            if (op == 12) r28::xdbl(acc);
+            if (op == 13) {
+                const r28::J28 j = r28::x_to_jac(acc);
+                put28(o, j.x);
+                put28(o + 14, j.y);
+                put28(o + 28, j.z);
+                break;
+            }
+            put28(o, acc.x);
+            put28(o + 14, acc.y);
+            put28(o + 28, acc.zz);
+            put28(o + 42, acc.zzz);
+            if (op == 10) o[56] = done ? 1u : 0u;
             break;
         }
         case 20: {

@@ -235,6 +235,93 @@ def _fq28_formulas(F, B16, B32, B512, ONE):
     return is_zero_mod, madd, mmadd, to_words
 
 
+def _xyzz_formulas(F, B16, B32, B512, ONE):
+    """r28::xdbl / xmadd / xmmadd / xadd / x_to_jac (XYZZ, mbls_fq28.hpp round 6) over the model F:
+    the same operations in the same order, each column checked below 2^64"""
+    is_zero_mod = _fq28_formulas(F, B16, B32, B512, ONE)[0]
+    P = F.P
+    ZERO = [0] * 14
+
+    def is_zero_lt2p(a):
+        return all(v == 0 for v in a) or all(v == p for v, p in zip(a, P))
+
+    def is_inf(acc):
+        return all(v == 0 for v in acc[2])
+
+    def xdbl(acc):
+        x, y, zz, zzz = acc
+        U = F.x2(y)
+        V = F.sqr(U)
+        W = F.mul(U, V)
+        S = F.mul(x, V)
+        A = F.sqr(x)
+        M = F.add(F.x2(A), A)
+        X3 = F.fold(F.sub(B32, F.sqr(M), F.x2(S)))
+        Y3 = F.mul2(M, F.sub(B16, S, X3), F.neg(B16, y), W)
+        return X3, Y3, F.mul(V, zz), F.mul(W, zzz)
+
+    def xmadd(acc, x2_, y2_):
+        if is_inf(acc):
+            return F.fold(x2_), F.fold(y2_), list(ONE), list(ONE)
+        x, y, zz, zzz = acc
+        U2 = F.mul(x2_, zz)
+        S2 = F.mul(y2_, zzz)
+        Pd = F.sub(B16, U2, x)
+        Rr = F.carry(F.sub(B16, S2, y))
+        PP = F.sqr(Pd)
+        if is_zero_lt2p(PP):
+            return xdbl(acc) if is_zero_mod(Rr) else (list(ONE), list(ONE), ZERO, ZERO)
+        ZZ3 = F.mul(zz, PP)
+        PPP = F.mul(Pd, PP)
+        ZZZ3 = F.mul(zzz, PPP)
+        Q = F.mul(x, PP)
+        X3 = F.fold(F.sub(B32, F.sub(B16, F.sqr(Rr), PPP), F.x2(Q)))
+        Y3 = F.mul2(Rr, F.sub(B16, Q, X3), F.neg(B16, y), PPP)
+        return X3, Y3, ZZ3, ZZZ3
+
+    def xmmadd(acc, x2_, y2_):
+        x, y = acc[0], acc[1]
+        Pd = F.fold(F.sub(B512, x2_, x))
+        PP = F.sqr(Pd)
+        if is_zero_lt2p(PP):
+            return None
+        Rr = F.fold(F.sub(B512, y2_, y))
+        PPP = F.mul(Pd, PP)
+        Q = F.mul(x, PP)
+        X3 = F.fold(F.sub(B32, F.sub(B16, F.sqr(Rr), PPP), F.x2(Q)))
+        Y3 = F.mul2(Rr, F.sub(B16, Q, X3), F.neg(B16, y), PPP)
+        return X3, Y3, PP, PPP
+
+    def xadd(acc, x2_, y2_, zz2, zzz2):
+        if is_inf(acc):
+            return F.fold(x2_), F.fold(y2_), F.fold(zz2), F.fold(zzz2)
+        x, y, zz, zzz = acc
+        U1 = F.mul(x, zz2)
+        U2 = F.mul(x2_, zz)
+        S1 = F.mul(y, zzz2)
+        S2 = F.mul(y2_, zzz)
+        Pd = F.sub(B16, U2, U1)
+        Rr = F.carry(F.sub(B16, S2, S1))
+        PP = F.sqr(Pd)
+        if is_zero_lt2p(PP):
+            return xdbl(acc) if is_zero_mod(Rr) else (list(ONE), list(ONE), ZERO, ZERO)
+        PPP = F.mul(Pd, PP)
+        Q = F.mul(U1, PP)
+        ZZ3 = F.mul(F.mul(zz, zz2), PP)
+        ZZZ3 = F.mul(F.mul(zzz, zzz2), PPP)
+        X3 = F.fold(F.sub(B32, F.sub(B16, F.sqr(Rr), PPP), F.x2(Q)))
+        Y3 = F.mul2(Rr, F.sub(B16, Q, X3), F.neg(B16, S1), PPP)
+        return X3, Y3, ZZ3, ZZZ3
+
+    def x_to_jac(acc):
+        if is_inf(acc):
+            return list(ONE), list(ONE), ZERO
+        x, y, zz, zzz = acc
+        return F.mul(x, F.sqr(zz)), F.mul(y, F.sqr(zzz)), list(zzz)
+
+    return xdbl, xmadd, xmmadd, xadd, x_to_jac
+
+
 class Model:
     """the GPU probe's interface (tests/diag/limbs_diag.hip op codes) over the limb model"""
 
@@ -242,14 +329,16 @@ class Model:
         self.F, self.G, self.Pint = Fq28(P, ninv, fold_recip), Fr29(R), P
         self.ONE = ONE
         self.is_zero_mod, self.madd, self.mmadd, self.to_words = _fq28_formulas(self.F, B16, B32, B512, ONE)
+        self.xdbl, self.xmadd, self.xmmadd, self.xadd, self.x_to_jac = _xyzz_formulas(self.F, B16, B32, B512, ONE)
 
     def __call__(self, op, cases):
         import numpy as np
-        out = np.zeros((len(cases), 48), dtype=np.uint64)
+        out = np.zeros((len(cases), 64), dtype=np.uint64)
         F, G = self.F, self.G
         for i, x in enumerate(cases):
-            x = [list(v) for v in x] + [[0] * 16] * (5 - len(x))
-            a, b, c, d, e = (v[:14] for v in x)
+            x = [list(v) for v in x] + [[0] * 16] * (8 - len(x))
+            a, b, c, d, e = (v[:14] for v in x[:5])
+            xs = [v[:14] for v in x]
             if op == 0:
                 r = F.mul(a, b)
             elif op == 1:
@@ -272,6 +361,17 @@ class Model:
                 r = [0] * 42 + [0] if res is None else res[0] + res[1] + res[2] + [1]
                 if res is None:  # acc untouched
                     r = a + b + list(self.ONE) + [0]
+            elif op == 9:  # xmadd(acc = x0..x3; q = x4, x5)
+                r = [v for c in self.xmadd(tuple(xs[:4]), xs[4], xs[5]) for v in c]
+            elif op == 10:  # xmmadd(acc = x0, x1, one, one; q = x4, x5): 56 words + the flag
+                res = self.xmmadd((xs[0], xs[1], None, None), xs[4], xs[5])
+                r = (xs[0] + xs[1] + list(self.ONE) * 2 + [0]) if res is None else [v for c in res for v in c] + [1]
+            elif op == 11:  # xadd(acc = x0..x3; partial = x4..x7)
+                r = [v for c in self.xadd(tuple(xs[:4]), *xs[4:8]) for v in c]
+            elif op == 12:  # xdbl(x0..x3)
+                r = [v for c in self.xdbl(tuple(xs[:4])) for v in c]
+            elif op == 13:  # x_to_jac(x0..x3): 42 words
+                r = [v for c in self.x_to_jac(tuple(xs[:4])) for v in c]
             elif op in (30, 31):
                 raise ValueError("pair ops: use run_pairs")
             elif op == 20:

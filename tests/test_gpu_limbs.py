@@ -440,3 +440,159 @@ def test_fq2_pair_madd_device(diag):
                 for j in range(2):
                     got = [int(v) for v in o[2 * i + j, 14 * k:14 * k + 14]]
                     assert got == exp[k][j], (op, i, k, j)
+
+
+# ----------------------------------------------------------------------------- XYZZ (round 6)
+def _aff_of_xyzz(X, Y, ZZ, ZZZ):
+    """plain affine point of an XYZZ quadruple of R'-form values (R' cancels in X / ZZ, Y / ZZZ)"""
+    if ZZ % P == 0:
+        return None
+    return (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P)
+
+
+def _aff_of_jac(X, Y, Z):
+    """plain affine point of R'-form Jacobian values"""
+    if Z % P == 0:
+        return None
+    zi = pow(Z, -1, P)
+    # R'-form values: x = (X R'^-1) / (Z R'^-1)^2 = X R' / Z^2
+    return (X * RP28 * zi * zi % P, Y * RP28 * RP28 * zi * zi * zi % P)
+
+
+def _rp(v):  # a field value into R'-form
+    return v * RP28 % P
+
+
+def _xyzz_of(pt, z, bump=0):
+    """pt (affine, plain) as XYZZ limbs with the implicit Z = z, R'-form, each coordinate lifted by
+    `bump` multiples of p (inside the < 3p invariant)"""
+    x, y = pt
+    vals = (x * z * z % P, y * z * z * z % P, z * z % P, z * z * z % P)
+    return [_limbs(_rp(v) + bump * P, 28, 14) for v in vals]
+
+
+def _q_unpacked(pt, negate):
+    """a base as the accumulation sees it: unpack_shift8 of its canonical Montgomery words
+    (x R' < 256 p); a negative digit takes y through neg<B512>"""
+    x, y = pt
+    qx, qy = unpack8(x * (1 << 384) % P), unpack8(y * (1 << 384) % P)
+    return qx, (neg(B512, qy) if negate else qy)
+
+
+def xyzz_cases():
+    """(acc, q, negate) on real G1 points: generic sums, the accumulator's coordinates lifted to their
+    invariant bounds, equal points (doubling), opposite points (infinity), an infinite accumulator"""
+    pts = [pr.g1_mul(k, pr.G1) for k in (1, 2, 3, 5, 1234567, 2 ** 200 + 7, pr.R - 1, 0xdeadbeef)]
+    cases = []
+    for i, a in enumerate(pts):
+        for j, b in enumerate(pts):
+            if i == j:
+                continue
+            z = rng.randrange(1, P)
+            cases.append((_xyzz_of(a, z, bump=(i + j) % 3), b, (i * j) % 2 == 1))
+    for k, a in enumerate(pts[:4]):
+        z = rng.randrange(1, P)
+        cases.append((_xyzz_of(a, z, bump=k % 3), a, False))   # equal: doubling
+        cases.append((_xyzz_of(a, z, bump=2), a, True))         # -a: infinity
+    cases.append(([list(ONE28), list(ONE28), [0] * 14, [0] * 14], pts[3], False))  # infinite accumulator
+    return cases
+
+
+def _check_xyzz_out(out, want, what):
+    rx, ry, rzz, rzzz = ([int(v) for v in out[14 * k:14 * k + 14]] for k in range(4))
+    got = _aff_of_xyzz(*(_val(c, 28) for c in (rx, ry, rzz, rzzz)))
+    assert got == want, what
+    if want is not None:
+        for c in (rx, ry, rzz, rzzz):
+            assert is_normalised(c) and _val(c, 28) < 3 * P, (what, "invariant")
+
+
+def test_xyzz_madd_mmadd_on_curve(diag):
+    """r28::xmadd / xmmadd (the G1 accumulation, round 6) on real points: the affine result equals
+    pyref's group law, including doubling / infinity on the exceptional branch, and the outputs
+    keep the accumulator invariant (normalised, < 3p); device and model alike"""
+    cases = xyzz_cases()
+    rows = []
+    for acc, b, ng in cases:
+        qx, qy = _q_unpacked(b, ng)
+        rows.append(acc + [qx, qy])
+    o = diag(9, rows)
+    for i, (acc, b, ng) in enumerate(cases):
+        a = _aff_of_xyzz(*(_val(c, 28) for c in acc))
+        bb = pr.g1_neg(b) if ng else b
+        _check_xyzz_out(o[i], bb if a is None else pr.g1_add(a, bb), ("xmadd", i))
+    # mmadd: the chunk's first point folded into acc (zz = zzz = R'-one)
+    mrows, mw = [], []
+    for acc, b, ng in cases[:-1]:
+        a = _aff_of_xyzz(*(_val(c, 28) for c in acc))
+        if a is None:
+            continue
+        x1, y1 = _limbs(_rp(a[0]) + P, 28, 14), _limbs(_rp(a[1]) + 2 * P, 28, 14)  # folded: < 3p
+        qx, qy = _q_unpacked(b, ng)
+        mrows.append([x1, y1, [0] * 14, [0] * 14, qx, qy])
+        mw.append((a, pr.g1_neg(b) if ng else b))
+    o = diag(10, mrows)
+    for i, (ap, bb) in enumerate(mw):
+        if ap[0] == bb[0]:
+            assert int(o[i, 56]) == 0, ("xmmadd must refuse x1 == x2", i)
+            continue
+        assert int(o[i, 56]) == 1
+        _check_xyzz_out(o[i], pr.g1_add(ap, bb), ("xmmadd", i))
+
+
+def test_xyzz_add_dbl_to_jac_on_curve(diag):
+    """r28::xadd (bucket sums of XYZZ partials), xdbl and x_to_jac on real points against pyref"""
+    pts = [pr.g1_mul(k, pr.G1) for k in (1, 2, 7, 99991, 2 ** 130 + 3, pr.R - 2)]
+    rows, want = [], []
+    for i, a in enumerate(pts):
+        for j, b in enumerate(pts):
+            za, zb = rng.randrange(1, P), rng.randrange(1, P)
+            acc = _xyzz_of(a, za, bump=(i + j) % 3)
+            # the partial as stored (canonical words) and unpacked: w 2^8 = v R'
+            part = [unpack8(_val(c, 28) % P * pow(1 << 8, -1, P) % P) for c in _xyzz_of(b, zb)]
+            rows.append(acc + part)
+            want.append(pr.g1_add(a, b))
+        za = rng.randrange(1, P)
+        rows.append(_xyzz_of(a, za, bump=1) + [unpack8(_val(c, 28) % P * pow(1 << 8, -1, P) % P)
+                                               for c in _xyzz_of(pr.g1_neg(a), rng.randrange(1, P))])
+        want.append(None)  # a + (-a)
+    o = diag(11, rows)
+    for i, w in enumerate(want):
+        _check_xyzz_out(o[i], w, ("xadd", i))
+    drows = [_xyzz_of(a, rng.randrange(1, P), bump=k % 3) for k, a in enumerate(pts)]
+    o = diag(12, drows)
+    for i, a in enumerate(pts):
+        _check_xyzz_out(o[i], pr.g1_add(a, a), ("xdbl", i))
+    o = diag(13, drows)
+    for i, a in enumerate(pts):
+        rx, ry, rz = ([int(v) for v in o[i, 14 * k:14 * k + 14]] for k in range(3))
+        assert _aff_of_jac(_val(rx, 28), _val(ry, 28), _val(rz, 28)) == a, ("x_to_jac", i)
+        assert all(v < (1 << 29) for v in rz[:-1]) and _val(rz, 28) < 8 * P  # J28's z invariant
+
+
+def xyzz_extreme_rows():
+    """limbs at the maxima the XYZZ formulas take (not curve points): accumulators at the invariant
+    bounds (all-MASK < 3p, 3p - 1, p), bases at the unpack / neg<B512> extremes"""
+    xs = [norm_max(3 * P), _limbs(3 * P - 1, 28, 14), _limbs(P, 28, 14)]
+    q = [unpack8(P - 1), unpack8(rng.randrange(P))]
+    rows9, rows11 = [], []
+    for k in range(27):
+        acc = [xs[k % 3], xs[(k // 3) % 3], xs[(k // 9) % 3], xs[(k + 1) % 3]]
+        qy = (unpack8(P - 1), neg(B512, [0] * 14), neg(B512, unpack8(P - 1)))[k % 3]
+        rows9.append(acc + [q[k % 2], qy])
+        rows11.append(acc + [unpack8(P - 1), q[k % 2], unpack8(P - 1), q[(k + 1) % 2]])
+    return rows9, rows11
+
+
+def test_xyzz_columns_at_limb_extremes(diag):
+    """the XYZZ formulas on limbs at their maxima: the model raises if any column reaches 2^64;
+    the device's limbs equal the model's bit for bit"""
+    import limbs_model
+    src = open(os.path.join(CSRC, "mbls_fq28.hpp")).read()
+    ninv = int(re.search(r"NINV = (0x[0-9a-f]+)u", src).group(1), 16)
+    M = limbs_model.Model(P, R, ninv, (1 << 40) // (0x1a011 + 1), B16, B32, B512, ONE28)
+    rows9, rows11 = xyzz_extreme_rows()
+    for op, rows in ((9, rows9), (10, rows9), (11, rows11), (12, rows9), (13, rows9)):
+        exp = M(op, rows)  # raises limbs_model.Overflow past a bound
+        got = diag(op, rows)
+        assert np.array_equal(np.asarray(got, dtype=np.uint64)[:, :57], exp[:, :57]), op
