@@ -204,6 +204,54 @@ __global__ __launch_bounds__(256, 3) void k_acc28_ceiling(const uint8_t* __restr
     clk_end(rec, c0, w0);
 }
 
+// the shipped G1 accumulation's arithmetic since round 6: XYZZ (r28::xmadd / xmmadd, y parked in
+// LDS), partials stored as 4 canonical coordinates (192 B)
+template <int CHUNK>
+__global__ __launch_bounds__(256, 3) void k_acc28x_ceiling(const uint8_t* __restrict__ table, uint8_t* __restrict__ partials,
+                                                           Clk* rec, uint32_t chunks_per_thread, uint32_t seed) {
+    unsigned long long c0, w0;
+    clk_begin(c0, w0);
+    __shared__ uint4 pts[PTS * 6];
+    __shared__ uint4 park[4 * 256];
+    for (int k = threadIdx.x; k < PTS * 6; k += blockDim.x) pts[k] = reinterpret_cast<const uint4*>(table)[k];
+    __syncthreads();
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t h = seed ^ (tid * 0x9e3779b9u);
+    for (uint32_t ch = 0; ch < chunks_per_thread; ++ch) {
+        r28::X28 acc = r28::X28::inf();
+        for (int e = 0; e < CHUNK; ++e) {
+            h = h * 1664525u + 1013904223u;
+            const uint32_t idx = (h >> 8) & (PTS - 1);
+            uint32_t xw[12], yw[12];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint4 xa = pts[idx * 6 + k], ya = pts[idx * 6 + 3 + k];
+                xw[4 * k] = xa.x, xw[4 * k + 1] = xa.y, xw[4 * k + 2] = xa.z, xw[4 * k + 3] = xa.w;
+                yw[4 * k] = ya.x, yw[4 * k + 1] = ya.y, yw[4 * k + 2] = ya.z, yw[4 * k + 3] = ya.w;
+            }
+            const r28::F28 qx = r28::unpack_shift8(xw);
+            r28::F28 qy = r28::unpack_shift8(yw);
+            if (h & 1) qy = r28::neg<r28::B512>(qy);
+            bool done = false;
+            if (e == 1 && !acc.is_inf()) done = r28::xmmadd(acc, qx, qy);
+            ParkLds pk{&park[threadIdx.x]};
+            if (!done) r28::xmadd(acc, qx, qy, pk);
+        }
+        uint4* q = reinterpret_cast<uint4*>(partials + ((size_t)tid * chunks_per_thread + ch) * 192);
+        auto put = [&](int k, const r28::F28& c) {
+            uint32_t w[12];
+            r28::to_words(c, w);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) q[3 * k + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+        };
+        put(0, acc.x);
+        put(1, acc.y);
+        put(2, acc.zz);
+        put(3, acc.zzz);
+    }
+    clk_end(rec, c0, w0);
+}
+
 // G2 (round 6): pair-sliced radix-2^28 Fq2, lane j of a pair holding component j; the table holds
 // 64 G2 points (192 B: x0 x1 y0 y1), each lane reading its component's words
 #ifndef MBLS_ACC_G2_MINW
@@ -455,6 +503,18 @@ int main(int argc, char** argv) {
                "\"contributions\": %.0f, \"ms\": %.4f, \"ns_per_contribution_chip\": %.6f, \"mhz_med\": %.0f, "
                "\"mhz_min\": %.0f, \"mhz_max\": %.0f, \"ms_per_2^20_g1_msm_contributions\": %.4f}",
                done, t28.ms, t28.ms * 1e6 / done, t28.mhz_med, t28.mhz_min, t28.mhz_max, t28.ms / done * 16777216.0);
+        uint8_t* d_part_x;
+        CK(hipMalloc(&d_part_x, (size_t)threads * per * 192));
+        auto L28x = [&] {
+            hipLaunchKernelGGL(k_acc28x_ceiling<16>, dim3(threads / 256), dim3(256), 0, 0, d_tab, d_part_x, d_rec, per, 99u);
+        };
+        Timing t28x = run(L28x, d_rec, threads / 64, 5);
+        CK(hipFree(d_part_x));
+        printf(",\n \"acc28x_ceiling\": {\"kernel\": \"k_acc28x_ceiling<16> (k_accumulate_r28 arithmetic since round 6: "
+               "XYZZ madd-2008-s in radix-2^28 Fq, y parked in LDS; points from LDS)\", "
+               "\"contributions\": %.0f, \"ms\": %.4f, \"ns_per_contribution_chip\": %.6f, \"mhz_med\": %.0f, "
+               "\"mhz_min\": %.0f, \"mhz_max\": %.0f, \"ms_per_2^20_g1_msm_contributions\": %.4f}",
+               done, t28x.ms, t28x.ms * 1e6 / done, t28x.mhz_med, t28x.mhz_min, t28x.mhz_max, t28x.ms / done * 16777216.0);
         // G2 pair-sliced: 2^(clog - 2) contributions (a G2 contribution costs ~3x a G1 one)
         {
             const size_t c2 = contributions / 4, chunks2 = c2 / 16;
