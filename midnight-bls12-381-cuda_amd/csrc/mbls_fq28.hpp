@@ -531,7 +531,8 @@ MBLS_DEV bool xmmadd(X28& acc, const F28& x2_, const F28& y2_) {
     return true;
 }
 
-// acc + a partial (x2, y2, zz2, zzz2), each from unpack_shift8 (< 256 p, normalised), zz2 != 0:
+// acc + a partial (x2, y2, zz2, zzz2), each normalised and < 256 p (unpack_shift8 of words, or a
+// stored accumulator's raw limbs: < 3p), zz2 != 0:
 // add-2008-s with the lazy Y3
 MBLS_DEV void xadd(X28& acc, const F28& x2_, const F28& y2_, const F28& zz2, const F28& zzz2) {
     if (acc.is_inf()) {

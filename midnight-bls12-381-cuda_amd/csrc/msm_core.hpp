@@ -321,32 +321,34 @@ __global__ __launch_bounds__(256, MINW) void k_accumulate(const uint32_t* __rest
 #ifndef MBLS_ACC_XYZZ
 #define MBLS_ACC_XYZZ 1  // G1 accumulation and light / slice-chain bucket sums in XYZZ (r28::X28)
 #endif
-// a chunk partial's bytes: G1 partials are XYZZ words (x, y, zz, zzz) when the accumulation runs in
-// XYZZ, Jacobian otherwise
+// a chunk partial's bytes: G1 partials are the accumulator's raw radix-2^28 XYZZ limbs when the
+// accumulation runs in XYZZ (4 x 14 words: no to_words conversion at the flush, which is divergent
+// -- a bucket boundary falls inside ~25% of the chunks, at a different step in every lane -- and no
+// unpack_shift8 when the bucket sums read them), Jacobian words otherwise
 template <class F>
 struct PartialBytes {
     static constexpr size_t value = 3 * sizeof(F);  // Jacobian
 };
 template <>
 struct PartialBytes<Fq> {
-    static constexpr size_t value = (MBLS_ACC_XYZZ && MBLS_ACC_R28 && MBLS_ACC_LDS && MBLS_BS_R28) ? 192 : 144;
+    static constexpr size_t value = (MBLS_ACC_XYZZ && MBLS_ACC_R28 && MBLS_ACC_LDS && MBLS_BS_R28) ? 224 : 144;
 };
 static_assert(!MBLS_ACC_XYZZ || (MBLS_ACC_R28 && MBLS_ACC_LDS && MBLS_BS_R28),
               "XYZZ partials need the radix-2^28 accumulation and bucket sums");
 MBLS_DEV void store_xyzz28(uint8_t* __restrict__ partials, uint32_t seg, const r28::X28& acc) {
-    uint4* q = reinterpret_cast<uint4*>(partials + (size_t)seg * 192);
-    const bool inf = acc.is_inf();
-    auto put = [&](int k, const r28::F28& c) {
-        uint32_t w[12];
-        r28::to_words(c, w);
+    // x, y folded (normalised, < 3p), zz, zzz normalised: valid xadd operands as they are; the
+    // identity is stored as zz = 0 (the reader's test)
+    uint4* q = reinterpret_cast<uint4*>(partials + (size_t)seg * 224);
+    uint32_t w[56];
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-            q[3 * k + j] = inf ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
-    };
-    put(0, acc.x);
-    put(1, acc.y);
-    put(2, acc.zz);
-    put(3, acc.zzz);
+    for (int i = 0; i < 14; ++i) {
+        w[i] = acc.x.l[i];
+        w[14 + i] = acc.y.l[i];
+        w[28 + i] = acc.zz.l[i];
+        w[42 + i] = acc.zzz.l[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 14; ++j) q[j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
 }
 MBLS_DEV void store_jac28(uint8_t* __restrict__ partials, uint32_t seg, const r28::J28& acc) {
     Jacobian<Fq> out;
@@ -795,22 +797,26 @@ MBLS_DEV bool load_j28(const uint8_t* __restrict__ base, size_t i, r28::F28& x, 
     return true;
 }
 // r28 XYZZ addition of chunk partial k (G1 with MBLS_ACC_XYZZ: the light path's and the slice
-// chains' form); the identity (zz = 0) adds nothing
+// chains' form; raw limbs, store_xyzz28); the identity (zz = 0) adds nothing
 MBLS_DEV void r28_add_partial(r28::X28& acc, const uint8_t* __restrict__ partials, uint32_t k) {
-    const uint4* q = reinterpret_cast<const uint4*>(partials + (size_t)k * 192);
-    uint32_t w[4][12], zany = 0;
+    const uint4* q = reinterpret_cast<const uint4*>(partials + (size_t)k * 224);
+    uint32_t w[56];
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int j = 0; j < 14; ++j) {
+        const uint4 u = q[j];
+        w[4 * j] = u.x, w[4 * j + 1] = u.y, w[4 * j + 2] = u.z, w[4 * j + 3] = u.w;
+    }
+    r28::F28 x, y, zz, zzz;
+    uint32_t zany = 0;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const uint4 u = q[3 * c + j];
-            w[c][4 * j] = u.x, w[c][4 * j + 1] = u.y, w[c][4 * j + 2] = u.z, w[c][4 * j + 3] = u.w;
-        }
-#pragma unroll
-    for (int j = 0; j < 12; ++j) zany |= w[2][j];
-    if (zany)
-        r28::xadd(acc, r28::unpack_shift8(w[0]), r28::unpack_shift8(w[1]), r28::unpack_shift8(w[2]),
-                  r28::unpack_shift8(w[3]));
+    for (int i = 0; i < 14; ++i) {
+        x.l[i] = w[i];
+        y.l[i] = w[14 + i];
+        zz.l[i] = w[28 + i];
+        zzz.l[i] = w[42 + i];
+        zany |= w[28 + i];
+    }
+    if (zany) r28::xadd(acc, x, y, zz, zzz);
 }
 // r28 lane addition of Jacobian chunk partial k (G1 without MBLS_ACC_XYZZ)
 MBLS_DEV void r28_add_partial(r28::J28& acc, const uint8_t* __restrict__ partials, uint32_t k) {
