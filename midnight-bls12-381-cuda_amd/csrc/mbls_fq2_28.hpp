@@ -127,6 +127,121 @@ MBLS_DEV bool mmadd(J28p& acc, const F28& x2_, const F28& y2_) {
     return true;
 }
 
+// ------------------------------------------------------------------------- XYZZ (round 6)
+// The G1 accumulation's XYZZ forms (mbls_fq28.hpp: madd-2008-s, add-2008-s, dbl-2008-s-1) over
+// pair-sliced Fq2: one squaring fewer per mixed addition (an r28 product per lane), two per full
+// addition.  Every product operand is carried first and every partner negation takes the bias
+// rule above; tests/limbs_model.py (_fq2_xyzz_formulas) restates each step and checks the columns.
+// Invariant between steps: x, y folded (normalised, < 3p); zz, zzz normalised, < 3p.
+struct X28p {
+    F28 x, y, zz, zzz;
+    MBLS_DEV bool is_inf() const {
+        uint32_t t = 0;
+#pragma unroll
+        for (int i = 0; i < r28::NL; ++i) t |= zz.l[i];
+        return both(t == 0);
+    }
+    MBLS_DEV static X28p inf() { return {one(), one(), F28::zero(), F28::zero()}; }
+};
+// the Fq2 value is 0 mod p (any components < 2^391)
+MBLS_DEV bool is_zero_mod(const F28& a) { return both(r28::is_zero_mod(a)); }
+
+MBLS_DEV void xdbl(X28p& a) {
+    using namespace r28;
+    const F28 U = carry(x2(a.y));  // < 6p
+    const F28 V = r28p::sqr<B16>(U);
+    const F28 W = r28p::mul<B16>(U, V);
+    const F28 S = r28p::mul<B16>(a.x, V);
+    const F28 A = r28p::sqr<B16>(a.x);
+    const F28 M = carry(add(x2(A), A));  // 3 X^2, < 6p
+    const F28 X3 = fold(sub<B32>(r28p::sqr<B16>(M), x2(S)));
+    a.y = r28p::mul2<B32, B16>(M, carry(sub<B16>(S, X3)), carry(neg<B16>(a.y)), W);
+    a.x = X3;
+    a.zz = r28p::mul<B16>(V, a.zz);
+    a.zzz = r28p::mul<B16>(W, a.zzz);
+}
+
+// acc + q (q = (x2, y2) from unpack_shift8, y2 carried after a negation; not the identity)
+MBLS_DEV void xmadd(X28p& acc, const F28& x2_, const F28& y2_) {
+    using namespace r28;
+    if (acc.is_inf()) {
+        acc = {fold(x2_), fold(y2_), one(), one()};
+        return;
+    }
+    const F28 U2 = r28p::mul<B16>(x2_, acc.zz);
+    const F28 S2 = r28p::mul<B16>(y2_, acc.zzz);
+    const F28 Pd = carry(sub<B16>(U2, acc.x));  // < 18p
+    const F28 R = carry(sub<B16>(S2, acc.y));   // < 18p
+    const F28 PP = r28p::sqr<B32>(Pd);
+    if (r28p::is_zero_lt2p(PP)) {  // equal or opposite points
+        if (r28p::is_zero_mod(R))
+            xdbl(acc);
+        else
+            acc = X28p::inf();
+        return;
+    }
+    acc.zz = r28p::mul<B16>(acc.zz, PP);
+    const F28 PPP = r28p::mul<B16>(Pd, PP);
+    acc.zzz = r28p::mul<B16>(acc.zzz, PPP);
+    const F28 Q = r28p::mul<B16>(acc.x, PP);
+    acc.x = fold(sub<B32>(sub<B16>(r28p::sqr<B32>(R), PPP), x2(Q)));
+    acc.y = r28p::mul2<B32, B16>(R, carry(sub<B16>(Q, acc.x)), carry(neg<B16>(acc.y)), PPP);
+}
+
+// acc fresh from the chunk's first point (zz = zzz = one, x, y folded) + q: ZZ = PP, ZZZ = PPP.
+// Returns false (acc untouched) when x1 == x2 mod p, left to xmadd's branches.
+MBLS_DEV bool xmmadd(X28p& acc, const F28& x2_, const F28& y2_) {
+    using namespace r28;
+    const F28 Pd = fold(sub<B512>(x2_, acc.x));
+    const F28 PP = r28p::sqr<B16>(Pd);
+    if (r28p::is_zero_lt2p(PP)) return false;
+    const F28 R = fold(sub<B512>(y2_, acc.y));
+    const F28 PPP = r28p::mul<B16>(Pd, PP);
+    const F28 Q = r28p::mul<B16>(acc.x, PP);
+    const F28 X3 = fold(sub<B32>(sub<B16>(r28p::sqr<B16>(R), PPP), x2(Q)));
+    acc.y = r28p::mul2<B32, B16>(R, carry(sub<B16>(Q, X3)), carry(neg<B16>(acc.y)), PPP);
+    acc.x = X3;
+    acc.zz = PP;
+    acc.zzz = PPP;
+    return true;
+}
+
+// acc + a partial (x2, y2, zz2, zzz2): a stored accumulator's raw limbs (normalised, < 3p), zz2 != 0
+MBLS_DEV void xadd(X28p& acc, const F28& x2_, const F28& y2_, const F28& zz2, const F28& zzz2) {
+    using namespace r28;
+    if (acc.is_inf()) {
+        acc = {x2_, y2_, zz2, zzz2};
+        return;
+    }
+    const F28 U1 = r28p::mul<B16>(acc.x, zz2);
+    const F28 U2 = r28p::mul<B16>(x2_, acc.zz);
+    const F28 S1 = r28p::mul<B16>(acc.y, zzz2);
+    const F28 S2 = r28p::mul<B16>(y2_, acc.zzz);
+    const F28 Pd = carry(sub<B16>(U2, U1));
+    const F28 R = carry(sub<B16>(S2, S1));
+    const F28 PP = r28p::sqr<B32>(Pd);
+    if (r28p::is_zero_lt2p(PP)) {
+        if (r28p::is_zero_mod(R))
+            xdbl(acc);
+        else
+            acc = X28p::inf();
+        return;
+    }
+    const F28 PPP = r28p::mul<B16>(Pd, PP);
+    const F28 Q = r28p::mul<B16>(U1, PP);
+    acc.zz = r28p::mul<B16>(r28p::mul<B16>(acc.zz, zz2), PP);
+    acc.zzz = r28p::mul<B16>(r28p::mul<B16>(acc.zzz, zzz2), PPP);
+    acc.x = fold(sub<B32>(sub<B16>(r28p::sqr<B32>(R), PPP), x2(Q)));
+    acc.y = r28p::mul2<B32, B16>(R, carry(sub<B16>(Q, acc.x)), carry(neg<B16>(S1)), PPP);
+}
+
+// XYZZ -> Jacobian (X ZZ^2, Y ZZZ^2, ZZZ)
+MBLS_DEV J28p x_to_jac(const X28p& a) {
+    using r28::B16;
+    if (a.is_inf()) return J28p::inf();
+    return {r28p::mul<B16>(a.x, r28p::sqr<B16>(a.zz)), r28p::mul<B16>(a.y, r28p::sqr<B16>(a.zzz)), a.zzz};
+}
+
 // this lane's component to / from the library's canonical Montgomery words (x R mod p)
 MBLS_DEV PFq2 to_pf(const F28& a) {
     PFq2 r;

@@ -333,6 +333,17 @@ template <>
 struct PartialBytes<Fq> {
     static constexpr size_t value = (MBLS_ACC_XYZZ && MBLS_ACC_R28 && MBLS_ACC_LDS && MBLS_BS_R28) ? 224 : 144;
 };
+#ifndef MBLS_ACC_G2_R28
+#define MBLS_ACC_G2_R28 1
+#endif
+#ifndef MBLS_ACC_G2_XYZZ
+#define MBLS_ACC_G2_XYZZ 1  // G2 accumulation and bucket sums in pair-sliced XYZZ (r28p::X28p), raw partials
+#endif
+#define MBLS_G2_XYZZ_PARTIALS (MBLS_ACC_G2_XYZZ && MBLS_ACC_G2_R28)
+template <>
+struct PartialBytes<Fq2> {
+    static constexpr size_t value = MBLS_G2_XYZZ_PARTIALS ? 448 : 288;
+};
 static_assert(!MBLS_ACC_XYZZ || (MBLS_ACC_R28 && MBLS_ACC_LDS && MBLS_BS_R28),
               "XYZZ partials need the radix-2^28 accumulation and bucket sums");
 MBLS_DEV void store_xyzz28(uint8_t* __restrict__ partials, uint32_t seg, const r28::X28& acc) {
@@ -513,6 +524,50 @@ __global__ __launch_bounds__(256, MBLS_ACC_R28_MINW) void k_accumulate_r28(const
 #ifndef MBLS_ACC_G2_LDS
 #define MBLS_ACC_G2_LDS 0  // 1: next point prefetched into LDS (LDS-DMA) instead of VGPRs
 #endif
+#ifndef MBLS_ACC_G2_XYZZ
+#define MBLS_ACC_G2_XYZZ 1  // G2 accumulation and bucket sums in pair-sliced XYZZ (r28p::X28p), raw partials
+#endif
+// G2 XYZZ partial k: lane j (component j) holds its 4 x 14 raw limbs at k * 448 + j * 224
+MBLS_DEV void store_xyzz28p(uint8_t* __restrict__ partials, uint32_t seg, const r28p::X28p& acc) {
+    uint4* q = reinterpret_cast<uint4*>(partials + (size_t)seg * 448 + (pairdpp::odd() ? 224 : 0));
+    uint32_t w[56];
+#pragma unroll
+    for (int i = 0; i < 14; ++i) {
+        w[i] = acc.x.l[i];
+        w[14 + i] = acc.y.l[i];
+        w[28 + i] = acc.zz.l[i];
+        w[42 + i] = acc.zzz.l[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 14; ++j) q[j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+}
+MBLS_DEV void r28p_add_partial(r28p::X28p& acc, const uint8_t* __restrict__ partials, uint32_t k) {
+    const uint4* q = reinterpret_cast<const uint4*>(partials + (size_t)k * 448 + (pairdpp::odd() ? 224 : 0));
+    uint32_t w[56];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+        const uint4 u = q[j];
+        w[4 * j] = u.x, w[4 * j + 1] = u.y, w[4 * j + 2] = u.z, w[4 * j + 3] = u.w;
+    }
+    r28::F28 x, y, zz, zzz;
+    uint32_t zany = 0;
+#pragma unroll
+    for (int i = 0; i < 14; ++i) {
+        x.l[i] = w[i];
+        y.l[i] = w[14 + i];
+        zz.l[i] = w[28 + i];
+        zzz.l[i] = w[42 + i];
+        zany |= w[28 + i];
+    }
+    // the identity is zz = 0 on both lanes (pair-uniform predicate)
+    if (!r28p::both(zany == 0)) r28p::xadd(acc, x, y, zz, zzz);
+}
+// pair XYZZ sum -> the library's Jacobian words of this lane's component
+MBLS_DEV Jacobian<PFq2> xyzz28p_to_words(const r28p::X28p& acc) {
+    const r28p::J28p j = r28p::x_to_jac(acc);
+    if (j.is_inf()) return Jacobian<PFq2>::inf();
+    return {r28p::to_pf(j.x), r28p::to_pf(j.y), r28p::to_pf(j.z)};
+}
 MBLS_DEV void store_jac28p(uint8_t* __restrict__ partials, uint32_t seg, const r28p::J28p& acc) {
     Jacobian<PFq2> out;
     if (acc.is_inf())
@@ -540,7 +595,19 @@ __global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_accumulate_r28p(const
     while (offsets[b + 1] <= beg) ++b;
     uint32_t seg = chunk_off[b] + (t - offsets[b] / chunk);
     uint32_t bend = offsets[b + 1];
-    r28p::J28p acc = r28p::J28p::inf();
+#if MBLS_ACC_G2_XYZZ
+    using Acc = r28p::X28p;
+#else
+    using Acc = r28p::J28p;
+#endif
+    Acc acc = Acc::inf();
+    auto flush = [&](uint32_t sg) __attribute__((always_inline)) {
+#if MBLS_ACC_G2_XYZZ
+        store_xyzz28p(partials, sg, acc);
+#else
+        store_jac28p(partials, sg, acc);
+#endif
+    };
 #if MBLS_ACC_G2_LDS
     // the next point's component (x: 3 x 16 B, y: 3 x 16 B per lane) prefetched into LDS by
     // LDS-DMA, double-buffered per wave (the G1 kernel's stage): no 24 VGPRs held across the
@@ -587,8 +654,8 @@ __global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_accumulate_r28p(const
         const Affine<PFq2> pn = fetch(vn);  // one point ahead: the gather overlaps this addition
 #endif
         if (e == bend) {  // bucket boundary inside the chunk: flush, move to the next bucket
-            store_jac28p(partials, seg, acc);
-            acc = r28p::J28p::inf();
+            flush(seg);
+            acc = Acc::inf();
             do {
                 ++b;
             } while (offsets[b + 1] == e);
@@ -599,6 +666,11 @@ __global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_accumulate_r28p(const
             const r28::F28 qx = r28::unpack_shift8(p.x.v.v);
             r28::F28 qy = r28::unpack_shift8(p.y.v.v);
             if (v & 1) qy = r28::carry(r28::neg<r28::B512>(qy));  // -P, normalised (mbls_fq2_28.hpp)
+#if MBLS_ACC_G2_XYZZ
+            bool done = false;
+            if (MBLS_ACC_MMADD && e == beg + 1 && !acc.is_inf()) done = r28p::xmmadd(acc, qx, qy);
+            if (!done) r28p::xmadd(acc, qx, qy);  // equal / opposite points: xdbl / identity inside
+#else
             if (acc.is_inf()) {
                 acc = {r28::fold(qx), r28::fold(qy), r28p::one()};
             } else {
@@ -616,6 +688,7 @@ __global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_accumulate_r28p(const
                                r28::fold(r28p::from_pf(aw.z))};
                 }
             }
+#endif
         }
 #if MBLS_ACC_G2_LDS
         v = vn;
@@ -625,7 +698,7 @@ __global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_accumulate_r28p(const
         p = pn;
 #endif
     }
-    store_jac28p(partials, seg, acc);
+    flush(seg);
 }
 
 // ------------------------------------------------------------------------------------
@@ -953,7 +1026,13 @@ MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t
             }
         } else {
             Jacobian<L> acc = Jacobian<L>::inf();
-            for (uint32_t k = c0 + j; k < c1; k += CHAINS) acc = jac_add(acc, load_jac<L>(partials, k));
+            if constexpr (std::is_same<F, Fq2>::value && MBLS_G2_XYZZ_PARTIALS) {
+                r28p::X28p xacc = r28p::X28p::inf();
+                for (uint32_t k = c0 + j; k < c1; k += CHAINS) r28p_add_partial(xacc, partials, k);
+                acc = xyzz28p_to_words(xacc);  // the lane tree below adds Jacobian chain sums
+            } else {
+                for (uint32_t k = c0 + j; k < c1; k += CHAINS) acc = jac_add(acc, load_jac<L>(partials, k));
+            }
             store_jac<L>(sh, j, acc);
             __syncthreads();
             for (; live > 16; live = (live + 1) / 2) {
@@ -1068,6 +1147,13 @@ __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32
         for (uint32_t k = k0; k < k1; ++k) r28_add_partial(acc, partials, k);
         store_jac28(buckets, b, acc);
 #endif
+        return;
+    }
+    if constexpr (std::is_same<F, Fq2>::value && MBLS_G2_XYZZ_PARTIALS) {
+        // pair-sliced radix-2^28 XYZZ sums of the raw XYZZ partials (round 6), one conversion
+        r28p::X28p acc = r28p::X28p::inf();
+        for (uint32_t k = k0; k < k1; ++k) r28p_add_partial(acc, partials, k);
+        store_jac<L>(buckets, b, xyzz28p_to_words(acc));
         return;
     }
     Jacobian<L> acc = Jacobian<L>::inf();

@@ -41,7 +41,7 @@ MBLS_DEV r29::F29 f29(const uint32_t* p) {
 //         8 mmadd(acc = x0, x1, one; q = x3, x4): 42 words + the flag
 //   XYZZ: 9 xmadd(acc = x0..x3; q = x4, x5): 56 words   10 xmmadd(acc = x0, x1, one, one; q = x4, x5):
 //         56 words + the flag   11 xadd(acc = x0..x3; partial x4..x7)   12 xdbl(x0..x3)
-//         13 x_to_jac(x0..x3): 42 words
+//         13 x_to_jac(x0..x3): 42 words   32-36: the pair-sliced forms of 9-13 (rows as 30 / 31)
 //  r29: 20 mul(x0, x1)   21 unpack(words x0)   22 pack(x0) (8 words)   23 mul_words(words x0, x1)
 //  pair-sliced Fq2 (mbls_fq2_28.hpp): rows 2i, 2i + 1 are the two lanes of case i (component 0, 1):
 //       30 madd(acc = x0, x1, x2; q = x3, x4): 42 words + the flag   31 mmadd(acc = x0, x1; q = x3, x4)
@@ -138,6 +138,31 @@ __global__ void k_limbs(int op, const uint32_t* __restrict__ in, uint32_t* __res
             put28(o + 14, acc.y);
             put28(o + 28, acc.z);
             o[42] = done ? 1u : 0u;
+            break;
+        }
+        case 32:
+        case 33:
+        case 34:
+        case 35:
+        case 36: {  // pair-sliced XYZZ (G2): as 9 / 10 / 11 / 12 / 13, rows 2i, 2i + 1 = the pair's lanes
+            r28p::X28p acc{f28(x), f28(x + 16), op == 33 ? r28p::one() : f28(x + 32), op == 33 ? r28p::one() : f28(x + 48)};
+            bool done = true;
+            if (op == 32) r28p::xmadd(acc, f28(x + 64), f28(x + 80));
+            if (op == 33) done = r28p::xmmadd(acc, f28(x + 64), f28(x + 80));
+            if (op == 34) r28p::xadd(acc, f28(x + 64), f28(x + 80), f28(x + 96), f28(x + 112));
+            if (op == 35) r28p::xdbl(acc);
+            if (op == 36) {
+                const r28p::J28p j = r28p::x_to_jac(acc);
+                put28(o, j.x);
+                put28(o + 14, j.y);
+                put28(o + 28, j.z);
+                break;
+            }
+            put28(o, acc.x);
+            put28(o + 14, acc.y);
+            put28(o + 28, acc.zz);
+            put28(o + 42, acc.zzz);
+            if (op == 33) o[56] = done ? 1u : 0u;
             break;
         }
         default: o[0] = 0xdeadbeefu; break;

@@ -503,3 +503,103 @@ def _fq2_formulas(F, B16, B32, B512, ONE):
         return X3, Y3, Z3
 
     return madd, mmadd
+
+
+def _fq2_xyzz_formulas(F, B16, B32, B512, ONE):
+    """the G2 accumulation's XYZZ forms over pair-sliced radix-2^28 Fq2 (csrc/mbls_fq2_28.hpp round
+    6: xdbl / xmadd / xmmadd / xadd / x_to_jac), step for step with their carries and biases"""
+    Q = Fq2P28(F, B16, B32, B512)
+    ONE2 = (list(ONE), [0] * 14)
+    ZERO2 = ([0] * 14, [0] * 14)
+    e = Q.each
+    Pint = sum(v << (28 * i) for i, v in enumerate(F.P))
+    is_zero_mod1 = _fq28_formulas(F, B16, B32, B512, ONE)[0]
+
+    def is_zero_lt2p(a):
+        for c in a:
+            if sum(v << (28 * i) for i, v in enumerate(c)) >= 2 * Pint:
+                raise Overflow("is_zero_lt2p: component >= 2p")
+        return all(all(v == 0 for v in c) or c == F.P for c in a)
+
+    def is_inf(acc):
+        return all(all(v == 0 for v in c) for c in acc[2])
+
+    def sub(bk):
+        return lambda a, b: F.sub(bk, a, b)
+
+    def xdbl(acc):
+        x, y, zz, zzz = acc
+        U = e(F.carry, e(F.x2, y))
+        V = Q.sqr(U, B16)
+        W = Q.mul(U, V, B16)
+        S = Q.mul(x, V, B16)
+        A = Q.sqr(x, B16)
+        M = e(F.carry, e(F.add, e(F.x2, A), A))
+        X3 = e(F.fold, e(sub(B32), Q.sqr(M, B16), e(F.x2, S)))
+        Y3 = Q.mul2(M, e(F.carry, e(sub(B16), S, X3)), e(F.carry, e(lambda a: F.neg(B16, a), y)), W, B32, B16)
+        return X3, Y3, Q.mul(V, zz, B16), Q.mul(W, zzz, B16)
+
+    def xmadd(acc, x2_, y2_):
+        if is_inf(acc):
+            return e(F.fold, x2_), e(F.fold, y2_), ONE2, ONE2
+        x, y, zz, zzz = acc
+        U2 = Q.mul(x2_, zz, B16)
+        S2 = Q.mul(y2_, zzz, B16)
+        Pd = e(F.carry, e(sub(B16), U2, x))
+        Rr = e(F.carry, e(sub(B16), S2, y))
+        PP = Q.sqr(Pd, B32)
+        if is_zero_lt2p(PP):
+            if all(is_zero_mod1(c) for c in Rr):
+                return xdbl(acc)
+            return ONE2, ONE2, ZERO2, ZERO2
+        ZZ3 = Q.mul(zz, PP, B16)
+        PPP = Q.mul(Pd, PP, B16)
+        ZZZ3 = Q.mul(zzz, PPP, B16)
+        Qv = Q.mul(x, PP, B16)
+        X3 = e(F.fold, e(sub(B32), e(sub(B16), Q.sqr(Rr, B32), PPP), e(F.x2, Qv)))
+        Y3 = Q.mul2(Rr, e(F.carry, e(sub(B16), Qv, X3)), e(F.carry, e(lambda a: F.neg(B16, a), y)), PPP, B32, B16)
+        return X3, Y3, ZZ3, ZZZ3
+
+    def xmmadd(acc, x2_, y2_):
+        x, y = acc[0], acc[1]
+        Pd = e(F.fold, e(sub(B512), x2_, x))
+        PP = Q.sqr(Pd, B16)
+        if is_zero_lt2p(PP):
+            return None
+        Rr = e(F.fold, e(sub(B512), y2_, y))
+        PPP = Q.mul(Pd, PP, B16)
+        Qv = Q.mul(x, PP, B16)
+        X3 = e(F.fold, e(sub(B32), e(sub(B16), Q.sqr(Rr, B16), PPP), e(F.x2, Qv)))
+        Y3 = Q.mul2(Rr, e(F.carry, e(sub(B16), Qv, X3)), e(F.carry, e(lambda a: F.neg(B16, a), y)), PPP, B32, B16)
+        return X3, Y3, PP, PPP
+
+    def xadd(acc, x2_, y2_, zz2, zzz2):
+        if is_inf(acc):
+            return x2_, y2_, zz2, zzz2
+        x, y, zz, zzz = acc
+        U1 = Q.mul(x, zz2, B16)
+        U2 = Q.mul(x2_, zz, B16)
+        S1 = Q.mul(y, zzz2, B16)
+        S2 = Q.mul(y2_, zzz, B16)
+        Pd = e(F.carry, e(sub(B16), U2, U1))
+        Rr = e(F.carry, e(sub(B16), S2, S1))
+        PP = Q.sqr(Pd, B32)
+        if is_zero_lt2p(PP):
+            if all(is_zero_mod1(c) for c in Rr):
+                return xdbl(acc)
+            return ONE2, ONE2, ZERO2, ZERO2
+        PPP = Q.mul(Pd, PP, B16)
+        Qv = Q.mul(U1, PP, B16)
+        ZZ3 = Q.mul(Q.mul(zz, zz2, B16), PP, B16)
+        ZZZ3 = Q.mul(Q.mul(zzz, zzz2, B16), PPP, B16)
+        X3 = e(F.fold, e(sub(B32), e(sub(B16), Q.sqr(Rr, B32), PPP), e(F.x2, Qv)))
+        Y3 = Q.mul2(Rr, e(F.carry, e(sub(B16), Qv, X3)), e(F.carry, e(lambda a: F.neg(B16, a), S1)), PPP, B32, B16)
+        return X3, Y3, ZZ3, ZZZ3
+
+    def x_to_jac(acc):
+        if is_inf(acc):
+            return ONE2, ONE2, ZERO2
+        x, y, zz, zzz = acc
+        return Q.mul(x, Q.sqr(zz, B16), B16), Q.mul(y, Q.sqr(zzz, B16), B16), zzz
+
+    return xdbl, xmadd, xmmadd, xadd, x_to_jac

@@ -596,3 +596,179 @@ def test_xyzz_columns_at_limb_extremes(diag):
         exp = M(op, rows)  # raises limbs_model.Overflow past a bound
         got = diag(op, rows)
         assert np.array_equal(np.asarray(got, dtype=np.uint64)[:, :57], exp[:, :57]), op
+
+
+# ----------------------------------------------------------------------------- pair-sliced XYZZ (G2)
+def _f2_rp(v):
+    return (v[0] * RP28 % P, v[1] * RP28 % P)
+
+
+def _xyzz2_of(pt, z, bump=0):
+    """G2 pt (affine, plain Fq2) as pair XYZZ limbs with the implicit Z = z: 4 tuples (c0, c1)"""
+    x, y = pt
+    z2 = pr.f2_mul(z, z)
+    z3 = pr.f2_mul(z2, z)
+    vals = (pr.f2_mul(x, z2), pr.f2_mul(y, z3), z2, z3)
+    return [tuple(_limbs(c + bump * P, 28, 14) for c in _f2_rp(v)) for v in vals]
+
+
+def _aff2(X, Y, ZZ, ZZZ):
+    """plain affine of pair XYZZ component values (R' cancels)"""
+    if ZZ[0] % P == 0 and ZZ[1] % P == 0:
+        return None
+    return (pr.f2_mul(X, pr.f2_inv(ZZ)), pr.f2_mul(Y, pr.f2_inv(ZZZ)))
+
+
+def _v2l(c):  # a pair of component limb lists -> component values
+    return (_val(c[0], 28), _val(c[1], 28))
+
+
+def _q2_unpacked(pt, negate):
+    """a G2 base as k_accumulate_r28p sees it: per component unpack_shift8 of the canonical
+    words; a negative digit: carry(neg<B512>(.)) per component"""
+    import limbs_model
+    F = limbs_model.Fq28(P, 0xffcfffd, (1 << 40) // (0x1a011 + 1))
+    x, y = pt
+    qx = tuple(unpack8(c * (1 << 384) % P) for c in x)
+    qy = tuple(unpack8(c * (1 << 384) % P) for c in y)
+    if negate:
+        qy = tuple(F.carry(F.neg(B512, c)) for c in qy)
+    return qx, qy
+
+
+def xyzz2_cases():
+    rz = lambda: (rng.randrange(P), rng.randrange(P))  # noqa: E731
+    pts = [pr.g2_mul(k, pr.G2) for k in (1, 2, 3, 77, 2 ** 100 + 9, pr.R - 1)]
+    cases = []
+    for i, a in enumerate(pts):
+        for j, b in enumerate(pts):
+            if i != j:
+                cases.append((_xyzz2_of(a, rz(), bump=(i + j) % 3), b, (i + j) % 2 == 1))
+    for k, a in enumerate(pts[:3]):
+        z = rz()
+        cases.append((_xyzz2_of(a, z, bump=k % 3), a, False))  # doubling
+        cases.append((_xyzz2_of(a, z, bump=1), a, True))        # infinity
+    return pts, cases
+
+
+def _check_xyzz2(out_pair, want, what):
+    """out_pair: (lane-0 limbs, lane-1 limbs) of the 4 coordinates"""
+    cs = [(out_pair[0][k], out_pair[1][k]) for k in range(4)]
+    got = _aff2(*(_v2l(c) for c in cs))
+    assert got == want, what
+    if want is not None:
+        for c in cs:
+            for comp in c:
+                assert is_normalised(comp) and _val(comp, 28) < 3 * P, (what, "invariant")
+
+
+def _pair_model():
+    import limbs_model
+    F = limbs_model.Fq28(P, 0xffcfffd, (1 << 40) // (0x1a011 + 1))
+    return limbs_model._fq2_xyzz_formulas(F, B16, B32, B512, ONE28)
+
+
+def _run_pair(diag, op, rows_per_case):
+    """device pair op: each case is a list of operand pairs (c0, c1); returns per case the 4 (or 3)
+    coordinates as (lane-0 list, lane-1 list) plus the flag"""
+    rows = []
+    for ops in rows_per_case:
+        for j in range(2):
+            rows.append([o[j] for o in ops])
+    o = diag(op, rows)
+    res = []
+    for i in range(len(rows_per_case)):
+        lanes = [[[int(v) for v in o[2 * i + j, 14 * k:14 * k + 14]] for k in range(4)] for j in range(2)]
+        res.append((lanes, int(o[2 * i, 56]), int(o[2 * i + 1, 56])))
+    return res
+
+
+def test_xyzz2_pair_on_curve_model():
+    """the pair-sliced XYZZ forms (tests/limbs_model.py _fq2_xyzz_formulas = csrc/mbls_fq2_28.hpp)
+    on real G2 points: affine results equal pyref's group law; no column reaches 2^64"""
+    xdbl, xmadd, xmmadd, xadd, x_to_jac = _pair_model()
+    pts, cases = xyzz2_cases()
+    for i, (acc, b, ng) in enumerate(cases):
+        qx, qy = _q2_unpacked(b, ng)
+        r = xmadd(tuple(acc), qx, qy)
+        a = _aff2(*(_v2l(c) for c in acc))
+        bb = pr.g2_neg(b) if ng else b
+        want = pr.g2_add(a, bb)
+        got = _aff2(*(_v2l(c) for c in r))
+        assert got == want, ("g2 xmadd", i)
+        if a is not None and a[0] != bb[0]:
+            x1 = tuple(_limbs(c + P, 28, 14) for c in _f2_rp(a[0]))
+            y1 = tuple(_limbs(c + 2 * P, 28, 14) for c in _f2_rp(a[1]))
+            r = xmmadd((x1, y1, None, None), qx, qy)
+            assert _aff2(*(_v2l(c) for c in r)) == want, ("g2 xmmadd", i)
+    for i, a in enumerate(pts):
+        for j, b in enumerate(pts):
+            r = xadd(tuple(_xyzz2_of(a, (rng.randrange(P), 5), bump=1)), *_xyzz2_of(b, (3, rng.randrange(P))))
+            assert _aff2(*(_v2l(c) for c in r)) == pr.g2_add(a, b), ("g2 xadd", i, j)
+        acc = tuple(_xyzz2_of(a, (rng.randrange(P), rng.randrange(P)), bump=2))
+        assert _aff2(*(_v2l(c) for c in xdbl(acc))) == pr.g2_add(a, a), ("g2 xdbl", i)
+        X, Y, Z = (_v2l(c) for c in x_to_jac(acc))
+        zi = pr.f2_inv(Z)
+        zi2 = pr.f2_mul(zi, zi)
+        # R'-form Jacobian: x = X R' / Z^2, y = Y R'^2 / Z^3
+        xa = pr.f2_mul(pr.f2_mul(X, zi2), (RP28 % P, 0))
+        ya = pr.f2_mul(pr.f2_mul(pr.f2_mul(Y, zi2), zi), (RP28 * RP28 % P, 0))
+        assert (xa, ya) == a, ("g2 x_to_jac", i)
+
+
+@pytest.mark.gpu
+def test_xyzz2_pair_device(diag):
+    """the device's pair-sliced XYZZ forms equal the model's limbs bit for bit, on G2 curve cases
+    and on accumulators at their invariant bounds (limb extremes)"""
+    import limbs_model
+    if isinstance(diag, limbs_model.Model):
+        pytest.skip("the model side is test_xyzz2_pair_on_curve_model")
+    xdbl, xmadd, xmmadd, xadd, x_to_jac = _pair_model()
+    pts, cases = xyzz2_cases()
+    ext = [norm_max(3 * P), _limbs(3 * P - 1, 28, 14), _limbs(P, 28, 14)]
+    rows9, exp9 = [], []
+    for acc, b, ng in cases:
+        qx, qy = _q2_unpacked(b, ng)
+        rows9.append(list(acc) + [qx, qy])
+    for k in range(9):  # extremes: every coordinate at an invariant bound, bases at the unpack maximum
+        acc = [(ext[k % 3], ext[(k + 1) % 3]), (ext[(k // 3) % 3], ext[k % 3]), (ext[(k + 2) % 3], ext[k % 3]),
+               (ext[(k // 3) % 3], ext[(k + 1) % 3])]
+        qx, qy = (unpack8(P - 1), unpack8(P - 1)), (unpack8(P - 1), unpack8(rng.randrange(P)))
+        rows9.append(acc + [qx, qy])
+    for ops in rows9:
+        exp9.append(xmadd(tuple(ops[:4]), ops[4], ops[5]))
+    for i, (lanes, _, _) in enumerate(_run_pair(diag, 32, rows9)):
+        for k in range(4):
+            assert (lanes[0][k], lanes[1][k]) == tuple(exp9[i][k]), ("xmadd", i, k)
+    rows11 = [list(_xyzz2_of(a, (rng.randrange(P), 7), bump=1)) + list(_xyzz2_of(b, (5, rng.randrange(P))))
+              for a in pts for b in pts]
+    for i, (lanes, _, _) in enumerate(_run_pair(diag, 34, rows11)):
+        exp = xadd(tuple(rows11[i][:4]), *rows11[i][4:])
+        for k in range(4):
+            assert (lanes[0][k], lanes[1][k]) == tuple(exp[k]), ("xadd", i, k)
+    rows12 = [list(_xyzz2_of(a, (rng.randrange(P), rng.randrange(P)), bump=k % 3)) for k, a in enumerate(pts)]
+    for i, (lanes, _, _) in enumerate(_run_pair(diag, 35, rows12)):
+        exp = xdbl(tuple(rows12[i]))
+        for k in range(4):
+            assert (lanes[0][k], lanes[1][k]) == tuple(exp[k]), ("xdbl", i, k)
+    for i, (lanes, _, _) in enumerate(_run_pair(diag, 36, rows12)):
+        exp = x_to_jac(tuple(rows12[i]))
+        for k in range(3):
+            assert (lanes[0][k], lanes[1][k]) == tuple(exp[k]), ("x_to_jac", i, k)
+    # mmadd: acc = (x1, y1) folded, zz = zzz = one (set by the op)
+    rows10 = []
+    for acc, b, ng in cases:
+        a = _aff2(*(_v2l(c) for c in acc))
+        if a is None:
+            continue
+        x1 = tuple(_limbs(c + P, 28, 14) for c in _f2_rp(a[0]))
+        y1 = tuple(_limbs(c + 2 * P, 28, 14) for c in _f2_rp(a[1]))
+        qx, qy = _q2_unpacked(b, ng)
+        rows10.append([x1, y1, ([0] * 14, [0] * 14), ([0] * 14, [0] * 14), qx, qy])
+    for i, (lanes, f0, f1) in enumerate(_run_pair(diag, 33, rows10)):
+        exp = xmmadd((rows10[i][0], rows10[i][1], None, None), rows10[i][4], rows10[i][5])
+        assert f0 == f1 == (0 if exp is None else 1), ("xmmadd flag", i)
+        if exp is None:
+            continue
+        for k in range(4):
+            assert (lanes[0][k], lanes[1][k]) == tuple(exp[k]), ("xmmadd", i, k)
