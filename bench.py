@@ -393,7 +393,7 @@ def main():
         _, pmc_src = pmc_summary()
         ceil = valu_ceiling() or {}
         # G1's accumulation is k_accumulate_r28 (round 5): its own arithmetic's ceiling when measured
-        acc_c = ceil.get("acc28_ceiling") or ceil.get("acc_ceiling") or {}
+        acc_c = ceil.get("acc28x_ceiling") or ceil.get("acc28_ceiling") or ceil.get("acc_ceiling") or {}
         # the shipped pass multiplies in radix 2^29 (round 6): its own body's ceiling when measured
         ntt_c = ceil.get("ntt29_ceiling") or ceil.get("ntt_ceiling") or {}
         isa = ceil.get("isa_2") or {}
@@ -451,8 +451,8 @@ def main():
                               "counter_issue_ms": round(acc_issue, 4) if acc_issue else None,
                               "counter_issue_frac": round(acc_issue / acc_ms, 4) if acc_issue and acc_ms else None,
                               "counter_source": f"{pmc_src} (SQ_INSTS_VALU per launch)" if pmc_src else None,
-                              "note": f"{contributions} mixed additions per launch; peak = k_acc28_ceiling "
-                                      "(tools/valu_ceiling.hip: the same radix-2^28 madd / mmadd code, launch bounds and chunk "
+                              "note": f"{contributions} mixed additions per launch; peak = k_acc28x_ceiling "
+                                      "(tools/valu_ceiling.hip: the same radix-2^28 XYZZ xmadd / xmmadd code, launch bounds and chunk "
                                       "structure with the points in LDS: no random gathers), measured on the box; "
                                       "frac = ceiling time / kernel time.  counter_issue_ms = the committed VALU "
                                       "instruction count at the measured cycles per wave-instruction and clock"},
@@ -733,7 +733,7 @@ def mix_leg(args, amd, torch, dev, rank, timed):
     acc_ms = g2_stage_ms(amd, torch, dev, g2, s_a)
     contributions = 4 * n * ((64 + 16 - 1) // 16)  # psi split: 4n digit streams x 4 windows (c = 16)
     ceil = valu_ceiling() or {}
-    g2c = ceil.get("acc28p_ceiling") or {}
+    g2c = ceil.get("acc28px_ceiling") or ceil.get("acc28p_ceiling") or {}
     g2_ceiling_ms = g2c["ms_per_2^20_g2_msm_contributions"] * contributions / 16777216.0 if g2c else None
     return {"g2_msm_points": n, "ntt_batch": B, "ntt_size": nn, "g2_msm_ms": round(g2_ms, 3),
             "g2_msm_per_sec": round(1e3 / g2_ms, 3),
@@ -750,8 +750,8 @@ def mix_leg(args, amd, torch, dev, rank, timed):
                                  "ceiling": g2c or None,
                                  "ceiling_source": ceil.get("source", "live: tools/valu_ceiling") if g2c else None,
                                  "note": f"{contributions} mixed additions per launch (psi split: 4n digit streams x 4 "
-                                         "windows); peak = k_acc28p_ceiling (tools/valu_ceiling.hip: the same "
-                                         "pair-sliced madd / mmadd and launch bounds with the points in LDS), "
+                                         "windows); peak = k_acc28px_ceiling (tools/valu_ceiling.hip: the same "
+                                         "pair-sliced XYZZ xmadd / xmmadd and launch bounds with the points in LDS), "
                                          "measured on the box; frac = ceiling time / kernel time"},
             "batched_ntt_ms": round(ntt_ms, 3), "overlapped_ms": round(both_ms, 3),
             "sum_isolated_ms": round(g2_ms + ntt_ms, 3), "streams": 2,

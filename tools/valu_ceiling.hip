@@ -298,6 +298,53 @@ __global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_acc28p_ceiling(const 
     clk_end(rec, c0, w0);
 }
 
+// the shipped G2 accumulation since round 6: pair-sliced XYZZ (r28p::xmadd / xmmadd), raw partials
+template <int CHUNK>
+__global__ __launch_bounds__(256, MBLS_ACC_G2_MINW) void k_acc28px_ceiling(const uint8_t* __restrict__ table,
+                                                                          uint8_t* __restrict__ partials, Clk* rec,
+                                                                          uint32_t chunks_per_pair, uint32_t seed) {
+    unsigned long long c0, w0;
+    clk_begin(c0, w0);
+    __shared__ uint4 pts[PTS * 12];
+    for (int k = threadIdx.x; k < PTS * 12; k += blockDim.x) pts[k] = reinterpret_cast<const uint4*>(table)[k];
+    __syncthreads();
+    const uint32_t pair = (blockIdx.x * blockDim.x + threadIdx.x) >> 1, j = threadIdx.x & 1;
+    uint32_t h = seed ^ (pair * 0x9e3779b9u);  // pair-uniform stream
+    for (uint32_t ch = 0; ch < chunks_per_pair; ++ch) {
+        r28p::X28p acc = r28p::X28p::inf();
+        for (int e = 0; e < CHUNK; ++e) {
+            h = h * 1664525u + 1013904223u;
+            const uint32_t idx = (h >> 8) & (PTS - 1);
+            uint32_t xw[12], yw[12];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint4 xa = pts[idx * 12 + 3 * j + k], ya = pts[idx * 12 + 6 + 3 * j + k];
+                xw[4 * k] = xa.x, xw[4 * k + 1] = xa.y, xw[4 * k + 2] = xa.z, xw[4 * k + 3] = xa.w;
+                yw[4 * k] = ya.x, yw[4 * k + 1] = ya.y, yw[4 * k + 2] = ya.z, yw[4 * k + 3] = ya.w;
+            }
+            const r28::F28 qx = r28::unpack_shift8(xw);
+            r28::F28 qy = r28::unpack_shift8(yw);
+            if (h & 1) qy = r28::carry(r28::neg<r28::B512>(qy));
+            bool done = false;
+            if (e == 1 && !acc.is_inf()) done = r28p::xmmadd(acc, qx, qy);
+            if (!done) r28p::xmadd(acc, qx, qy);
+        }
+        // raw limbs, as k_accumulate_r28p stores its XYZZ partials (store_xyzz28p)
+        uint4* q = reinterpret_cast<uint4*>(partials + ((size_t)pair * chunks_per_pair + ch) * 448 + 224 * j);
+        uint32_t w[56];
+#pragma unroll
+        for (int i = 0; i < 14; ++i) {
+            w[i] = acc.x.l[i];
+            w[14 + i] = acc.y.l[i];
+            w[28 + i] = acc.zz.l[i];
+            w[42 + i] = acc.zzz.l[i];
+        }
+#pragma unroll
+        for (int k = 0; k < 14; ++k) q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    }
+    clk_end(rec, c0, w0);
+}
+
 // --------------------------------------------------------------------- k_ntt_pass body ceiling
 __constant__ uint32_t TWO_R[8] = {0x00000002u, 0xfffffffeu, 0xfffcb7fdu, 0xa77b4805u,
                                   0x1343b00au, 0x6673b010u, 0x533afa90u, 0xe7db4ea6u};
@@ -537,6 +584,17 @@ int main(int argc, char** argv) {
                    "pair-sliced radix-2^28 Fq2; points from LDS)\", \"contributions\": %.0f, \"ms\": %.4f, "
                    "\"ns_per_contribution_chip\": %.6f, \"mhz_med\": %.0f, \"ms_per_2^20_g2_msm_contributions\": %.4f}",
                    done2, tg.ms, tg.ms * 1e6 / done2, tg.mhz_med, tg.ms / done2 * 16777216.0);
+            uint8_t* d_part2x;
+            CK(hipMalloc(&d_part2x, (size_t)pairs * per2 * 448));
+            auto LG2x = [&] {
+                hipLaunchKernelGGL(k_acc28px_ceiling<16>, dim3(threads / 256), dim3(256), 0, 0, d_tab2, d_part2x, d_rec, per2, 77u);
+            };
+            Timing tgx = run(LG2x, d_rec, threads / 64, 5);
+            printf(",\n \"acc28px_ceiling\": {\"kernel\": \"k_acc28px_ceiling<16> (k_accumulate_r28p<G2> arithmetic since round 6: "
+                   "pair-sliced radix-2^28 XYZZ; points from LDS)\", \"contributions\": %.0f, \"ms\": %.4f, "
+                   "\"ns_per_contribution_chip\": %.6f, \"mhz_med\": %.0f, \"ms_per_2^20_g2_msm_contributions\": %.4f}",
+                   done2, tgx.ms, tgx.ms * 1e6 / done2, tgx.mhz_med, tgx.ms / done2 * 16777216.0);
+            CK(hipFree(d_part2x));
             CK(hipFree(d_tab2));
             CK(hipFree(d_part2));
         }
