@@ -334,6 +334,16 @@ int mbls_profile_read(const char** names, double* total_ms, long* counts, int ma
 eIcicleError mbls_msm_accumulate_event(void* stream, void* event);
 eIcicleError mbls_msm_accumulate_event_drop(void* event);
 
+/* precompute_factor guard (no reference counterpart).  The reference's plain
+ * device-bases MSMs pass MIDNIGHT_GPU_PRECOMPUTE as precompute_factor with n PLAIN bases
+ * (core/msm.rs:897-913).  Default: a device allocation too short for n x F entries runs as plain
+ * bases (a sub-allocated buffer of a larger pool is not caught).  Strict (on != 0, process-wide):
+ * precompute_factor > 1 is honoured only for a table this library's precompute_bases wrote to
+ * device memory (same pointer, same factor, entries covering the call) and every other buffer
+ * runs as plain bases -- exact for pooled buffers; a table assembled elsewhere (copied or
+ * concatenated) then needs precompute_factor = 1 semantics or its own precompute_bases call. */
+eIcicleError mbls_msm_precompute_strict(int on);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,7 +77,7 @@ EXPORTED = [
     "mbls_release_stream", "mbls_release_scratch", "mbls_scratch_stats",
     "mbls_g1_msm_multi_device", "mbls_g2_msm_multi_device", "bls12_381_vector_sum",
     "bls12_381_g1_affine_to_projective", "bls12_381_g1_projective_to_affine", "bls12_381_g2_projective_to_affine",
-    "mbls_msm_plan", "mbls_msm_accumulate_event", "mbls_msm_accumulate_event_drop",
+    "mbls_msm_plan", "mbls_msm_accumulate_event", "mbls_msm_accumulate_event_drop", "mbls_msm_precompute_strict",
 ]
 
 _LIB = None
@@ -122,6 +122,7 @@ def lib():
         "bls12_381_g2_projective_to_affine": [P, i32, P, P],
         "mbls_msm_plan": [i32, i32, P, P],
         "mbls_msm_accumulate_event": [P, P], "mbls_msm_accumulate_event_drop": [P],
+        "mbls_msm_precompute_strict": [i32],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -479,3 +480,9 @@ def torch_u64(shape_or_array, device="cuda"):
 
 def to_numpy_u64(t):
     return t.detach().cpu().numpy().view(np.uint64)
+
+
+def msm_precompute_strict(on=True):
+    """mbls_msm_precompute_strict: precompute_factor > 1 only for tables precompute_bases wrote
+    (include/bls12_381_mi355x.h); process-wide"""
+    check(lib().mbls_msm_precompute_strict(1 if on else 0), "mbls_msm_precompute_strict")

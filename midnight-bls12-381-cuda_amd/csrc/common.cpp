@@ -252,6 +252,49 @@ size_t device_bytes_from(const void* p) {
     return q >= b && q <= b + size ? (size_t)(b + size - q) : SIZE_MAX;
 }
 
+// ---- precompute_bases tables (ADVICE / VERDICT r5: the plain-bases guard) ------------------
+// precompute_call registers every table it writes; with strict mode on, an MSM takes
+// precompute_factor > 1 only for a registered table whose factor matches and whose entries cover
+// the call, and runs anything else as plain bases (factor 1).  Bounded: the oldest of
+// PRECOMP_SLOTS registrations is forgotten first (re-running precompute_bases registers again).
+namespace {
+struct PrecompEntry {
+    const void* p = nullptr;
+    size_t bytes = 0;
+    int factor = 0, device = -1;
+};
+constexpr int PRECOMP_SLOTS = 256;
+std::mutex g_precomp_mu;
+PrecompEntry g_precomp[PRECOMP_SLOTS];
+int g_precomp_next = 0;
+std::atomic<int> g_precomp_strict{0};
+}  // namespace
+
+void precompute_register(const void* table, size_t bytes, int factor) {
+    int dev = -1;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_precomp_mu);
+    for (auto& e : g_precomp)
+        if (e.p == table && e.device == dev) {  // the same buffer rewritten: replace
+            e = {table, bytes, factor, dev};
+            return;
+        }
+    g_precomp[g_precomp_next] = {table, bytes, factor, dev};
+    g_precomp_next = (g_precomp_next + 1) % PRECOMP_SLOTS;
+}
+
+bool precompute_strict() { return g_precomp_strict.load(std::memory_order_relaxed) != 0; }
+void precompute_set_strict(bool on) { g_precomp_strict.store(on ? 1 : 0, std::memory_order_relaxed); }
+
+bool precompute_is_table(const void* bases, int factor, size_t want_bytes) {
+    int dev = -1;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_precomp_mu);
+    for (const auto& e : g_precomp)
+        if (e.p && e.p == bases && e.device == dev && e.factor == factor && want_bytes <= e.bytes) return true;
+    return false;
+}
+
 bool is_device_pointer(const void* p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -317,6 +360,10 @@ hipEvent_t take_accumulate_event(hipStream_t st) {
 }  // namespace mbls
 
 extern "C" {
+eIcicleError mbls_msm_precompute_strict(int on) {
+    mbls::precompute_set_strict(on != 0);
+    return MBLS_SUCCESS;
+}
 
 void mbls_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(mbls::g_prof_mu);

@@ -116,6 +116,11 @@ const void* pinned_host_device_pointer(const void* p);
 // bytes from `p` to the end of the device allocation holding it (hipMemGetAddressRange), or
 // SIZE_MAX when the runtime cannot tell (host memory, foreign allocators)
 size_t device_bytes_from(const void* p);
+// precompute_bases tables written by this library (common.cpp): registration, strict mode, lookup
+void precompute_register(const void* table, size_t bytes, int factor);
+bool precompute_strict();
+void precompute_set_strict(bool on);
+bool precompute_is_table(const void* bases, int factor, size_t want_bytes);
 // the event mbls_msm_accumulate_event left pending for `st` (taken: nullptr afterwards), or nullptr
 hipEvent_t take_accumulate_event(hipStream_t st);
 // a taken accumulate event: recorded on `st` when the guard dies unless release()d first (the

@@ -1990,12 +1990,16 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     // never reads the factor.  A device allocation too short for n x F table entries cannot be a
     // precompute_bases table: it runs as factor 1, the reference's result (the
     // binding should pass PrecomputedBases::factor()).
+    // Strict mode (mbls_msm_precompute_strict(1), for a binding that cannot pass the table's own
+    // factor): only a table precompute_bases wrote (registered, same factor, covering the call)
+    // runs as a table; anything else is plain bases -- exact for sub-allocated buffers too.
     MSMConfig cfg_plain;
     if (cfg->precompute_factor > 1 && cfg->are_points_on_device && bases && msm_size > 0) {
         const bool sh = cfg->are_points_shared_in_batch || batch == 1;
         const size_t want = (size_t)msm_size * (size_t)cfg->precompute_factor * (sh ? 1 : (size_t)batch) *
                             GroupTraits<F>::AFF;
-        if (device_bytes_from(bases) < want) {
+        if (precompute_strict() ? !precompute_is_table(bases, cfg->precompute_factor, want)
+                                : device_bytes_from(bases) < want) {
             cfg_plain = *cfg;
             cfg_plain.precompute_factor = 1;
             cfg = &cfg_plain;
@@ -2265,6 +2269,7 @@ eIcicleError precompute_call(const void* in, int n, const MSMConfig* cfg, void* 
     MBLS_TRY(hipGetLastError());
     MBLS_TRY(hipMemcpyAsync(out, dout, out_b, cfg->are_results_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
     MBLS_TRY(hipStreamSynchronize(st));
+    if (cfg->are_results_on_device) precompute_register(out, out_b, factor);  // strict mode's table list
     return MBLS_SUCCESS;
 }
 

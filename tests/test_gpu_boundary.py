@@ -245,6 +245,39 @@ def test_precompute_factor_on_plain_device_bases(amd, gh, hip, group):
         raw.free()
 
 
+@pytest.mark.parametrize("group", ["g1", "g2"])
+def test_precompute_factor_pooled_plain_bases(amd, gh, group):
+    """n plain bases in a sub-buffer of a larger pooled allocation (a caching
+    allocator's segment) with precompute_factor 4.  Default mode: the allocation heuristic cannot
+    tell them from a table -- pinned here as the KNOWN limitation (the result is not the plain
+    MSM).  Strict mode (mbls_msm_precompute_strict): only tables precompute_bases wrote run as
+    tables, so the pooled plain bases give the plain result, while a registered table still
+    gives the table result."""
+    import torch
+    n, w, F = 2048, (12 if group == "g1" else 24), 4
+    pool = torch.zeros((6 * n, w), dtype=torch.int64, device="cuda")  # one segment, several buffers
+    plain = pool[n:2 * n]
+    amd.gen_bases(group, plain, 0x5EED0B71)
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 0x5EED0B72, montgomery=True)
+    torch.cuda.synchronize()
+    ref = amd.msm(group, s, plain, scalars_mont=True, n=n)
+    table = torch.zeros((n * F, w), dtype=torch.int64, device="cuda")
+    amd.precompute_bases(group, plain, F, n, out=table)
+    try:
+        r = amd.msm(group, s, plain, scalars_mont=True, precompute_factor=F, n=n)
+        assert not np.array_equal(r, ref), "default mode: pooled plain bases read as a table (known)"
+        amd.msm_precompute_strict(True)
+        r = amd.msm(group, s, plain, scalars_mont=True, precompute_factor=F, n=n)
+        assert np.array_equal(r, ref), "strict mode: pooled plain bases run as plain"
+        r = amd.msm(group, s, table, scalars_mont=True, points_mont=False, precompute_factor=F, n=n)
+        assert np.array_equal(r, ref), "strict mode: a registered table still runs as a table"
+        r = amd.msm(group, s, table[n:], scalars_mont=True, precompute_factor=F, n=n // 2)
+        assert gh.decode_icicle(group, r[0]) is not None  # an unregistered pointer: plain, no fault
+    finally:
+        amd.msm_precompute_strict(False)
+
+
 def test_msm_accumulate_event_orders_a_second_stream(amd, gh):
     """mbls_msm_accumulate_event (config #5's overlap): the next MSM on the stream records the
     event once its accumulation is enqueued; an NTT on another stream waits on it.  Both results
