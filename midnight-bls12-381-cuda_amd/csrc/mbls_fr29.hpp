@@ -104,5 +104,44 @@ MBLS_DEV F29 mul(const F29& a, const F29& b) {
 // [0, 2r) as words when x is x R, w is w R' (see the header)
 MBLS_DEV Fr mul_words(const Fr& x, const F29& w) { return pack(mul(unpack(x), w)); }
 
+// two independent products a b, c d column by column, their mad chains interleaved
+// (madc::col2): the same values as two mul() calls.  Measured in tools/valu_ceiling.hip
+// (k_ntt29x_ceiling): no faster than two mul() calls at 4-5 waves per SIMD (the mad latency is
+// already hidden), so the NTT pass does not use it (profiles/r06/README.md)
+template <int K>
+MBLS_DEV void mul2x_cols(uint64_t& p, uint32_t (&m)[NL], F29& r, const F29& a, const F29& b, uint64_t& q,
+                         uint32_t (&n)[NL], F29& t, const F29& c, const F29& d) {
+    if constexpr (K < 2 * NL - 1) {
+        constexpr int LO = K > NL - 1 ? K - (NL - 1) : 0;
+        madc::col2<K, LO, (K < NL - 1 ? K : NL - 1), false>(p, a.l, b.l, q, c.l, d.l);
+        madc::col2<K, LO, (K < NL ? K : NL) - 1, true>(p, m, RL, q, n, RL);
+        if constexpr (K < NL) {
+            m[K] = (0u - (uint32_t)p) & MASK;
+            n[K] = (0u - (uint32_t)q) & MASK;
+            p += m[K];
+            q += n[K];
+        } else {
+            r.l[K - NL] = (uint32_t)p & MASK;
+            t.l[K - NL] = (uint32_t)q & MASK;
+        }
+        p >>= 29;
+        q >>= 29;
+        mul2x_cols<K + 1>(p, m, r, a, b, q, n, t, c, d);
+    }
+}
+MBLS_DEV void mul2x(F29& r, const F29& a, const F29& b, F29& t, const F29& c, const F29& d) {
+    uint32_t m[NL], n[NL];
+    uint64_t p = 0, q = 0;
+    mul2x_cols<0>(p, m, r, a, b, q, n, t, c, d);
+    r.l[NL - 1] = (uint32_t)p;
+    t.l[NL - 1] = (uint32_t)q;
+}
+MBLS_DEV void mul_words2x(Fr& x, const F29& w, Fr& y, const F29& v) {
+    F29 r, t;
+    mul2x(r, unpack(x), w, t, unpack(y), v);
+    x = pack(r);
+    y = pack(t);
+}
+
 }  // namespace r29
 }  // namespace mbls

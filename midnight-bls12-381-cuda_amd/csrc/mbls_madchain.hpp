@@ -92,5 +92,58 @@ MBLS_DEV void col(uint64_t& acc, const X& x, const Y& y) {
     }
 }
 
+// Two independent columns (A, B) interleaved inside one statement: A0 B0 A1 B1 ... -- each chain's
+// dependent mads are two instructions apart, so a wave waits half as long on the 64-bit mad
+// latency (round 6: two products of a butterfly / an addition that do not depend on each other)
+#define MBLS_MADX_STEP(ACC, A, B) "v_mad_u64_u32 " ACC ", %2, " A ", " B ", " ACC "\n\t"
+template <bool S>
+MBLS_DEV void madx1(uint64_t& p, uint64_t& q, uint32_t a0, uint32_t b0, uint32_t c0, uint32_t d0) {
+    uint64_t c;
+    if constexpr (S)
+        asm(MBLS_MADX_STEP("%0", "%3", "%4") MBLS_MADX_STEP("%1", "%5", "%6")
+            : "+v"(p), "+v"(q), "=&s"(c) : "v"(a0), "s"(b0), "v"(c0), "s"(d0));
+    else
+        asm(MBLS_MADX_STEP("%0", "%3", "%4") MBLS_MADX_STEP("%1", "%5", "%6")
+            : "+v"(p), "+v"(q), "=&s"(c) : "v"(a0), "v"(b0), "v"(c0), "v"(d0));
+}
+template <bool S>
+MBLS_DEV void madx4(uint64_t& p, uint64_t& q, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2,
+                    uint32_t b2, uint32_t a3, uint32_t b3, uint32_t c0, uint32_t d0, uint32_t c1, uint32_t d1,
+                    uint32_t c2, uint32_t d2, uint32_t c3, uint32_t d3) {
+    uint64_t c;
+#define MBLS_MADX_4                                                                                                \
+    MBLS_MADX_STEP("%0", "%3", "%4") MBLS_MADX_STEP("%1", "%11", "%12") MBLS_MADX_STEP("%0", "%5", "%6")             \
+        MBLS_MADX_STEP("%1", "%13", "%14") MBLS_MADX_STEP("%0", "%7", "%8") MBLS_MADX_STEP("%1", "%15", "%16")       \
+            MBLS_MADX_STEP("%0", "%9", "%10") MBLS_MADX_STEP("%1", "%17", "%18")
+    if constexpr (S)
+        asm(MBLS_MADX_4
+            : "+v"(p), "+v"(q), "=&s"(c)
+            : "v"(a0), "s"(b0), "v"(a1), "s"(b1), "v"(a2), "s"(b2), "v"(a3), "s"(b3), "v"(c0), "s"(d0), "v"(c1),
+              "s"(d1), "v"(c2), "s"(d2), "v"(c3), "s"(d3));
+    else
+        asm(MBLS_MADX_4
+            : "+v"(p), "+v"(q), "=&s"(c)
+            : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(c0), "v"(d0), "v"(c1),
+              "v"(d1), "v"(c2), "v"(d2), "v"(c3), "v"(d3));
+#undef MBLS_MADX_4
+}
+#undef MBLS_MADX_STEP
+
+// p += sum_{i = I..HI} x[i] y[K - i], q += the same over (u, v): one interleaved chain pair
+template <int K, int I, int HI, bool S, class X, class Y>
+MBLS_DEV void col2(uint64_t& p, const X& x, const Y& y, uint64_t& q, const X& u, const Y& v) {
+    if constexpr (I <= HI) {
+        constexpr int R = HI - I + 1;
+        if constexpr (R >= 4) {
+            madx4<S>(p, q, x[I], y[K - I], x[I + 1], y[K - I - 1], x[I + 2], y[K - I - 2], x[I + 3], y[K - I - 3], u[I],
+                     v[K - I], u[I + 1], v[K - I - 1], u[I + 2], v[K - I - 2], u[I + 3], v[K - I - 3]);
+            col2<K, I + 4, HI, S>(p, x, y, q, u, v);
+        } else {
+            madx1<S>(p, q, x[I], y[K - I], u[I], v[K - I]);
+            col2<K, I + 1, HI, S>(p, x, y, q, u, v);
+        }
+    }
+}
+
 }  // namespace madc
 }  // namespace mbls

@@ -442,6 +442,47 @@ __global__ __launch_bounds__(256, 5) void k_ntt29_ceiling(const uint8_t* __restr
     clk_end(rec, c0, w0);
 }
 
+// round 6: the same body with each butterfly's two independent products interleaved
+// (r29::mul_words2x: their mad chains alternate inside the asm statements)
+template <int MINW>
+__global__ __launch_bounds__(256, MINW) void k_ntt29x_ceiling(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                              Clk* rec, int iters) {
+    unsigned long long c0, w0;
+    clk_begin(c0, w0);
+    __shared__ uint4 twa[256], twb[256];
+    __shared__ uint32_t twc[256];
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) {
+        const r29::F29 t = r29::unpack(load<FrCfg>(in + 32 * k));
+        twa[k] = make_uint4(t.l[0], t.l[1], t.l[2], t.l[3]);
+        twb[k] = make_uint4(t.l[4], t.l[5], t.l[6], t.l[7]);
+        twc[k] = t.l[8];
+    }
+    __syncthreads();
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    Fr x0 = load<FrCfg>(in + 32 * ((tid + 1) & 255)), x1 = load<FrCfg>(in + 32 * ((tid + 2) & 255)),
+       x2 = load<FrCfg>(in + 32 * ((tid + 3) & 255)), x3 = load<FrCfg>(in + 32 * ((tid + 4) & 255));
+    auto ldw = [&](uint32_t g) {
+        const uint4 a = twa[g], b = twb[g];
+        return r29::F29{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, twc[g]}};
+    };
+    for (int i = 0; i < iters; ++i) {
+        const uint32_t j = (tid + 3u * i) & 127u;
+        const r29::F29 w1 = ldw(j), w2 = ldw(j + 64), w3 = ldw(j + 128);
+        r29::mul_words2x(x1, w1, x3, w1);
+        Fr y0 = add2r(x0, x1), y1 = sub2r(x0, x1), y2 = add2r(x2, x3), y3 = sub2r(x2, x3);
+        r29::mul_words2x(y2, w2, y3, w3);
+        x0 = add2r(y0, y2);
+        x2 = sub2r(y0, y2);
+        x1 = add2r(y1, y3);
+        x3 = sub2r(y1, y3);
+    }
+    store<FrCfg>(out + 128 * (size_t)tid, x0);
+    store<FrCfg>(out + 128 * (size_t)tid + 32, x1);
+    store<FrCfg>(out + 128 * (size_t)tid + 64, x2);
+    store<FrCfg>(out + 128 * (size_t)tid + 96, x3);
+    clk_end(rec, c0, w0);
+}
+
 // ------------------------------------------------------------------------------------ host
 struct Timing {
     double ms, mhz_med, mhz_min, mhz_max, wave_cycles_med;
@@ -627,6 +668,19 @@ int main(int argc, char** argv) {
                "products, twiddle limb planes from LDS)\", \"radix4_butterflies\": %.0f, \"ms\": %.4f, "
                "\"G_radix4_per_s\": %.3f, \"mhz_med\": %.0f, \"ms_per_2^22_transform_10_pairs\": %.4f}",
                bf, t29.ms, bf / (t29.ms * 1e-3) / 1e9, t29.mhz_med, 10.0 * (1 << 20) / (bf / (t29.ms * 1e-3)) * 1e3);
+        for (int mw = 5; mw >= 4; --mw) {
+            auto L29x = [&] {
+                if (mw == 5)
+                    hipLaunchKernelGGL(k_ntt29x_ceiling<5>, dim3(nb), dim3(256), 0, 0, d_in, d_o, d_rec, it);
+                else
+                    hipLaunchKernelGGL(k_ntt29x_ceiling<4>, dim3(nb), dim3(256), 0, 0, d_in, d_o, d_rec, it);
+            };
+            Timing t29x = run(L29x, d_rec, (size_t)nb * 4, 5);
+            printf(",\n \"ntt29x%d_ceiling\": {\"kernel\": \"k_ntt29x_ceiling<%d> (the radix-4 body with each butterfly's two "
+                   "independent products interleaved, r29::mul_words2x; %d waves per SIMD)\", \"radix4_butterflies\": %.0f, \"ms\": %.4f, "
+                   "\"G_radix4_per_s\": %.3f, \"mhz_med\": %.0f, \"ms_per_2^22_transform_10_pairs\": %.4f}",
+                   mw, mw, mw, bf, t29x.ms, bf / (t29x.ms * 1e-3) / 1e9, t29x.mhz_med, 10.0 * (1 << 20) / (bf / (t29x.ms * 1e-3)) * 1e3);
+        }
         CK(hipFree(d_in));
         CK(hipFree(d_o));
     }
