@@ -346,6 +346,19 @@ struct PartialBytes<Fq2> {
 };
 static_assert(!MBLS_ACC_XYZZ || (MBLS_ACC_R28 && MBLS_ACC_LDS && MBLS_BS_R28),
               "XYZZ partials need the radix-2^28 accumulation and bucket sums");
+#ifndef MBLS_RED_R28
+#define MBLS_RED_R28 1  // G1's lane-mode reduction levels in radix 2^28 (k_reduce_scaled_r28)
+#endif
+#ifndef MBLS_BUCKETS_XYZZ
+#define MBLS_BUCKETS_XYZZ 1  // G1: the bucket sums stay raw XYZZ (224 B) for a lane-mode level 0
+#endif
+// G1 with a lane-mode level 0 (every large MSM): k_bucket_small stores the bucket sums as raw XYZZ
+// limbs (store_xyzz28) and level 0 adds them in XYZZ (k_reduce_scaled_r28x): no x_to_jac per
+// bucket, add-2008-s instead of add-2007-bl in the level's chains, no unpack_shift8 on its loads
+template <class F>
+constexpr bool buckets_xyzz_ok() {
+    return std::is_same<F, Fq>::value && MBLS_ACC_XYZZ && MBLS_RED_R28 && MBLS_BUCKETS_XYZZ;
+}
 MBLS_DEV void store_xyzz28(uint8_t* __restrict__ partials, uint32_t seg, const r28::X28& acc) {
     // x, y folded (normalised, < 3p), zz, zzz normalised: valid xadd operands as they are; the
     // identity is stored as zz = 0 (the reader's test)
@@ -926,9 +939,40 @@ MBLS_DEV void r28_add_partial(r28::J28& acc, const uint8_t* __restrict__ partial
 #endif
 static constexpr uint32_t HEAVY_SLICE_MIN = MBLS_HEAVY_SLICE_MIN, HEAVY_LDS = 1024, HEAVY_GROUP = 16;
 
+// a bucket's row-layout sum (limb j on lane j of row 0 -- wave layout's leader row, or the row
+// tree's row 0) into `buckets`: Jacobian words (rstore_jac), or with xb the raw XYZZ limbs of
+// (X, Y, Z^2, Z^3) the lane-mode level 0 reads (k_reduce_scaled_r28x).  Wave 0, all 64 lanes.
+template <class F>
+MBLS_DEV void store_bucket_row(uint8_t* __restrict__ buckets, uint32_t b, const RJac<F>& p, bool xb) {
+    if constexpr (buckets_xyzz_ok<F>()) {
+        if (xb) {
+            uint32_t w[3][12], zany = 0;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+                w[0][i] = (uint32_t)__shfl((int)p.x.v, i, 64);
+                w[1][i] = (uint32_t)__shfl((int)p.y.v, i, 64);
+                w[2][i] = (uint32_t)__shfl((int)p.z.v, i, 64);
+                zany |= w[2][i];
+            }
+            if (threadIdx.x != 0) return;
+            r28::X28 a = r28::X28::inf();
+            if (zany) {
+                const r28::F28 z = r28::unpack_shift8(w[2]);
+                a.x = r28::fold(r28::unpack_shift8(w[0]));
+                a.y = r28::fold(r28::unpack_shift8(w[1]));
+                a.zz = r28::sqr(z);
+                a.zzz = r28::mul(a.zz, z);
+            }
+            store_xyzz28(buckets, b, a);
+            return;
+        }
+    }
+    if (wave::leader_row()) rstore_jac<F>(buckets, b, p);
+}
+
 template <class F>
 MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t* __restrict__ partials,
-                           uint8_t* __restrict__ buckets, const HeavyTab& H, uint32_t hb, uint32_t nhb) {
+                           uint8_t* __restrict__ buckets, const HeavyTab& H, uint32_t hb, uint32_t nhb, bool xb) {
     using L = typename LaneOf<F>::type;
     using IO = RedIO<F, MODE_ROW>;
     constexpr uint32_t LN = LaneOf<F>::LANES;
@@ -1083,12 +1127,12 @@ MBLS_DEV void heavy_slices(const uint32_t* __restrict__ chunk_off, const uint8_t
 #endif
             if (nsum <= 16) {  // workgroup-uniform
                 const RJac<F> tot = wave_sum16<F>(sh, nsum, [&](uint32_t k) { return WIO::ld(H.res, f0 + k * step); });
-                if (threadIdx.x < 64) WIO::st(buckets, b, tot);
+                if (threadIdx.x < 64) store_bucket_row<F>(buckets, b, tot, xb);
             } else {
                 RJac<F> tot = r < nsum ? IO::ld(H.res, f0 + r * step) : RJac<F>::inf();
                 for (uint32_t k = r + 16; k < nsum; k += 16) tot = IO::add(tot, IO::ld(H.res, f0 + k * step));
                 tot = row_tree<F>(tot, sh, r);
-                if (threadIdx.x < 16) IO::st(buckets, b, tot);
+                if (threadIdx.x < 64) store_bucket_row<F>(buckets, b, tot, xb);
             }
 #if MBLS_HEAVY_TRACE
             const uint64_t trb = wall_clock64();
@@ -1117,13 +1161,14 @@ template <class F>
 __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32_t* __restrict__ chunk_off,
                                                       const uint32_t* __restrict__ perm, const uint32_t* __restrict__ binbase,
                                                       uint32_t gwords, const uint8_t* __restrict__ partials,
-                                                      uint8_t* __restrict__ buckets, uint32_t light_blocks, HeavyTab H) {
+                                                      uint8_t* __restrict__ buckets, uint32_t light_blocks, HeavyTab H,
+                                                      int xb) {
     MBLS_TAIL_PRIO();
     using L = typename LaneOf<F>::type;
     // the slice workgroups come first: dispatched at once, the heavy buckets' chains overlap the
     // light buckets (they used to start behind them: G1 2^20 half ones ~0.1 ms)
     if (blockIdx.x < HEAVY_BLOCKS) {
-        heavy_slices<F>(chunk_off, partials, buckets, H, blockIdx.x, HEAVY_BLOCKS);
+        heavy_slices<F>(chunk_off, partials, buckets, H, blockIdx.x, HEAVY_BLOCKS, xb != 0);
         return;
     }
     // light workgroups one wave-priority step below the slice workgroups: the heavy buckets'
@@ -1141,7 +1186,10 @@ __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32
 #if MBLS_ACC_XYZZ
         r28::X28 acc = r28::X28::inf();
         for (uint32_t k = k0; k < k1; ++k) r28_add_partial(acc, partials, k);
-        store_jac28(buckets, b, r28::x_to_jac(acc));
+        if (xb)
+            store_xyzz28(buckets, b, acc);
+        else
+            store_jac28(buckets, b, r28::x_to_jac(acc));
 #else
         r28::J28 acc = r28::J28::inf();
         for (uint32_t k = k0; k < k1; ++k) r28_add_partial(acc, partials, k);
@@ -1218,9 +1266,6 @@ __global__ __launch_bounds__(256) void k_reduce_scaled(const uint8_t* __restrict
 // G1's lane-mode level in radix 2^28 (round 5: the same outputs as k_reduce_scaled<Fq,
 // MODE_LANE> -- jadd / dbl compute the field values of jac_add / jac_dbl -- with ~20% fewer
 // instructions per addition on a chain that runs one wave per SIMD)
-#ifndef MBLS_RED_R28
-#define MBLS_RED_R28 1
-#endif
 template <class F>  // F = Fq only
 __global__ __launch_bounds__(256) void k_reduce_scaled_r28(const uint8_t* __restrict__ V, const uint8_t* __restrict__ U,
                                                            uint32_t m_in, uint32_t seg_log, int Wg, int off,
@@ -1246,6 +1291,33 @@ __global__ __launch_bounds__(256) void k_reduce_scaled_r28(const uint8_t* __rest
         store_jac28(Vout, tid, R);
     }
     store_jac28(Uout, tid, S);
+}
+
+// level 0 over raw XYZZ buckets (buckets_xyzz_ok, no U): the chain of k_reduce_scaled_r28 with
+// add-2008-s (r28::xadd, 12M + 2S) for its two additions per step, the outputs converted once
+template <class F>  // F = Fq only
+__global__ __launch_bounds__(256) void k_reduce_scaled_r28x(const uint8_t* __restrict__ V, uint32_t m_in,
+                                                            uint32_t seg_log, int Wg, int off,
+                                                            uint8_t* __restrict__ Vout, uint8_t* __restrict__ Uout) {
+    MBLS_TAIL_PRIO();
+    const uint32_t seg = 1u << seg_log;
+    const uint32_t m_out = (m_in + seg - 1) >> seg_log;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= m_out * (uint32_t)Wg) return;
+    const uint32_t w = tid / m_out, q = tid % m_out;
+    const uint32_t k0 = q << seg_log;
+    const uint32_t k1 = min(k0 + seg, m_in);  // exclusive
+    const uint32_t base = w * m_in;
+    r28::X28 R = r28::X28::inf(), S = r28::X28::inf();
+    for (uint32_t t = k1; t-- > k0;) {
+        r28_add_partial(R, V, base + t);                                                   // R += V_t
+        if ((t - k0) + off != 0 && !R.is_inf()) r28::xadd(S, R.x, R.y, R.zz, R.zzz);  // S += R
+    }
+    if (Vout) {
+        for (uint32_t k = 0; k < seg_log; ++k) r28::xdbl(R);
+        store_jac28(Vout, tid, r28::x_to_jac(R));
+    }
+    store_jac28(Uout, tid, r28::x_to_jac(S));
 }
 
 // A narrow level (few segments: the GPU is idle but for one wave per chain) as a tree: one
@@ -1604,7 +1676,14 @@ struct MsmScratchSizes {
 #endif
 inline uint32_t wave_min_chains(bool fq2 = false) { return fq2 ? MBLS_WAVE_MIN_G2 : MBLS_WAVE_MIN; }
 
-inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks, size_t part) {
+// raw XYZZ buckets for this plan (buckets_xyzz_ok, level 0 in lanes)
+template <class F>
+inline bool buckets_xyzz(const MsmPlan& P) {
+    return buckets_xyzz_ok<F>() && P.levels > 0 && P.mode[0] == MODE_LANE;
+}
+// bkt: a bucket sum's bytes (jac, or 224 for raw XYZZ buckets)
+inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks, size_t part,
+                                         size_t bkt) {
     MsmScratchSizes z;
     // the per-call image table; with bstride > 1 also the compact copy of the points (2n rows)
     z.phi = P.split > 1 && !P.prepared ? align_up(P.pts / P.split * (P.split - 1 + (P.bstride > 1 ? 1 : 0)) * aff) : 0;
@@ -1644,7 +1723,7 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     z.owner = align_up((size_t)max_chunks * 4);
     z.first = align_up((NC / P.chunk + 2) * 4);
     z.partials = align_up((size_t)max_chunks * part);  // part: a chunk partial's bytes (PartialBytes)
-    z.buckets = align_up((size_t)P.TB * jac);
+    z.buckets = align_up((size_t)P.TB * bkt);
     // V / U ping-pong halves sized for the widest level's outputs (k_reduce_scaled)
     const size_t mo0 = P.levels ? (P.level_m[0] + P.seg(0) - 1) / P.seg(0) : 1;
     z.levelT = align_up(2 * mo0 * P.Wg * jac);
@@ -1778,7 +1857,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     const uint32_t TB = P.TB;
     const size_t NC = P.contributions;
     const uint32_t max_chunks = (uint32_t)(NC / P.chunk + TB + 1);
-    MsmScratchSizes z = msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value);
+    const bool xb = buckets_xyzz<F>(P);
+    MsmScratchSizes z = msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value, xb ? 224 : JAC);
     uint32_t* keys = (uint32_t*)arena.take(z.keys);
     uint32_t* vals = (uint32_t*)arena.take(z.vals);
     uint32_t* ranks = (uint32_t*)arena.take(z.ranks);
@@ -1920,7 +2000,7 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         const uint32_t light_blocks = (TB * LN + 255) / 256;
         if (pipe && pipe->reuse) MBLS_TRY(hipStreamWaitEvent(st, pipe->reuse, 0));
         hipLaunchKernelGGL(k_bucket_small<F>, dim3(light_blocks + HEAVY_BLOCKS), dim3(256), 0, st, chunk_off, perm, binbase,
-                           order_words(TB), partials, buckets, light_blocks, H);
+                           order_words(TB), partials, buckets, light_blocks, H, xb ? 1 : 0);
     }
     if (pipe) {  // the tail moves to the side stream
         MBLS_TRY(hipEventRecord(pipe->bucket_done, st));
@@ -1942,8 +2022,17 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             const bool last = l == P.levels - 1;
             uint8_t* Vo = last ? nullptr : vb[l & 1];
             uint8_t* Uo = last ? windows : ub[l & 1];
-            launch_reduce_scaled<F>(P.mode[l], V, U, m_in, P.seg_log[l], P.Wg, l == 0 ? 1 : 0, Vo, Uo,
-                                    m_out * (uint32_t)P.Wg, st);
+            bool done = false;
+            if constexpr (buckets_xyzz_ok<F>()) {
+                if (l == 0 && xb) {
+                    hipLaunchKernelGGL((k_reduce_scaled_r28x<F>), dim3((m_out * (uint32_t)P.Wg + 255) / 256), dim3(256),
+                                       0, st, V, m_in, P.seg_log[0], P.Wg, 1, Vo, Uo);
+                    done = true;
+                }
+            }
+            if (!done)
+                launch_reduce_scaled<F>(P.mode[l], V, U, m_in, P.seg_log[l], P.Wg, l == 0 ? 1 : 0, Vo, Uo,
+                                        m_out * (uint32_t)P.Wg, st);
             V = Vo;
             U = Uo;
         }
@@ -2029,7 +2118,8 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
         fprintf(stderr, "[mbls] msm n=%d c=%d W=%d Wg=%d split=%d TB=%u contributions=%zu chunk=%u levels=%d\n", msm_size,
                 P.c, P.W, P.Wg, P.split, P.TB, P.contributions, P.chunk, P.levels);
     uint32_t max_chunks = (uint32_t)(P.contributions / P.chunk + P.TB + 1);
-    size_t scratch = msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value).total();
+    size_t scratch =
+        msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value, buckets_xyzz<F>(P) ? 224 : JAC).total();
     const bool piped = batch > 1 && batch_pipe() > 0;
     er = lease.reserve(st_s + st_b + st_r + scratch * (piped ? 2 : 1) + 4096);
     if (er != MBLS_SUCCESS) return er;
