@@ -216,6 +216,10 @@ namespace mbls {
 #ifndef MBLS_LANE_LEVELS
 #define MBLS_LANE_LEVELS 1
 #endif
+// segment log of the lane levels after level 0 (variant builds: short chains, many lanes)
+#ifndef MBLS_SEGL_LOG
+#define MBLS_SEGL_LOG MBLS_SEG0_LOG
+#endif
 eIcicleError plan_levels(MsmPlan& p, int Wl) {
     constexpr int row_log = MBLS_ROW_SEG_LOG, row_log_g2 = MBLS_ROW_SEG_LOG_G2, seg0_log = MBLS_SEG0_LOG,
                   wave_log = MBLS_WSEG_LOG, lane_levels = MBLS_LANE_LEVELS;
@@ -227,8 +231,9 @@ eIcicleError plan_levels(MsmPlan& p, int Wl) {
     uint32_t m = p.B;
     while (true) {
         if (p.levels >= MAX_LEVELS) return MBLS_INVALID_ARGUMENT;
-        int lg = seg0_log, mode = MODE_LANE;
-        const uint32_t lane_chains = ((m + (1u << seg0_log) - 1) >> seg0_log) * (uint32_t)Wl;
+        const int ll = p.levels == 0 ? seg0_log : MBLS_SEGL_LOG;
+        int lg = ll, mode = MODE_LANE;
+        const uint32_t lane_chains = ((m + (1u << ll) - 1) >> ll) * (uint32_t)Wl;
         if (p.levels >= lane_levels || lane_chains < lane_min) {
             const int rl = p.fq2 ? row_log_g2 : row_log;
             const uint32_t row_chains = ((m + (1u << rl) - 1) >> rl) * (uint32_t)Wl;
