@@ -220,6 +220,18 @@ namespace mbls {
 #ifndef MBLS_SEGL_LOG
 #define MBLS_SEGL_LOG MBLS_SEG0_LOG
 #endif
+// the same three for G2: two more lane levels of 2-input segments (the FIPS pair chain) from 8192
+// chains instead of wave-layout levels -- G2 2^20 9.36 / 9.37 -> 9.23 / 9.16 ms
+// (profiles/r06/ab/g2_lane_levels_ab.txt; G1 within 1%, lane_levels_ab.txt)
+#ifndef MBLS_LANE_LEVELS_G2
+#define MBLS_LANE_LEVELS_G2 3
+#endif
+#ifndef MBLS_SEGL_LOG_G2
+#define MBLS_SEGL_LOG_G2 1
+#endif
+#ifndef MBLS_LANE_MIN_G2
+#define MBLS_LANE_MIN_G2 8192u
+#endif
 eIcicleError plan_levels(MsmPlan& p, int Wl) {
     constexpr int row_log = MBLS_ROW_SEG_LOG, row_log_g2 = MBLS_ROW_SEG_LOG_G2, seg0_log = MBLS_SEG0_LOG,
                   wave_log = MBLS_WSEG_LOG, lane_levels = MBLS_LANE_LEVELS;
@@ -231,10 +243,12 @@ eIcicleError plan_levels(MsmPlan& p, int Wl) {
     uint32_t m = p.B;
     while (true) {
         if (p.levels >= MAX_LEVELS) return MBLS_INVALID_ARGUMENT;
-        const int ll = p.levels == 0 ? seg0_log : MBLS_SEGL_LOG;
+        const int ll = p.levels == 0 ? seg0_log : p.fq2 ? MBLS_SEGL_LOG_G2 : MBLS_SEGL_LOG;
         int lg = ll, mode = MODE_LANE;
         const uint32_t lane_chains = ((m + (1u << ll) - 1) >> ll) * (uint32_t)Wl;
-        if (p.levels >= lane_levels || lane_chains < lane_min) {
+        const int lanes_to = p.fq2 ? MBLS_LANE_LEVELS_G2 : lane_levels;
+        const uint32_t lmin = (p.levels > 0 && p.fq2) ? MBLS_LANE_MIN_G2 : lane_min;
+        if (p.levels >= lanes_to || lane_chains < lmin) {
             const int rl = p.fq2 ? row_log_g2 : row_log;
             const uint32_t row_chains = ((m + (1u << rl) - 1) >> rl) * (uint32_t)Wl;
             mode = row_chains >= wave_min_chains(p.fq2) ? MODE_ROW : MODE_WAVE;

@@ -352,12 +352,20 @@ static_assert(!MBLS_ACC_XYZZ || (MBLS_ACC_R28 && MBLS_ACC_LDS && MBLS_BS_R28),
 #ifndef MBLS_BUCKETS_XYZZ
 #define MBLS_BUCKETS_XYZZ 1  // G1: the bucket sums stay raw XYZZ (224 B) for a lane-mode level 0
 #endif
+#ifndef MBLS_BUCKETS_XYZZ_G2
+#define MBLS_BUCKETS_XYZZ_G2 1  // G2: the same, pair-sliced (448 B)
+#endif
 // G1 with a lane-mode level 0 (every large MSM): k_bucket_small stores the bucket sums as raw XYZZ
 // limbs (store_xyzz28) and level 0 adds them in XYZZ (k_reduce_scaled_r28x): no x_to_jac per
 // bucket, add-2008-s instead of add-2007-bl in the level's chains, no unpack_shift8 on its loads
 template <class F>
 constexpr bool buckets_xyzz_ok() {
-    return std::is_same<F, Fq>::value && MBLS_ACC_XYZZ && MBLS_RED_R28 && MBLS_BUCKETS_XYZZ;
+    return (std::is_same<F, Fq>::value && MBLS_ACC_XYZZ && MBLS_RED_R28 && MBLS_BUCKETS_XYZZ) ||
+           (std::is_same<F, Fq2>::value && MBLS_G2_XYZZ_PARTIALS && MBLS_BUCKETS_XYZZ_G2);
+}
+template <class F>
+constexpr size_t xyzz_bucket_bytes() {
+    return std::is_same<F, Fq>::value ? 224 : 448;
 }
 MBLS_DEV void store_xyzz28(uint8_t* __restrict__ partials, uint32_t seg, const r28::X28& acc) {
     // x, y folded (normalised, < 3p), zz, zzz normalised: valid xadd operands as they are; the
@@ -573,6 +581,19 @@ MBLS_DEV void r28p_add_partial(r28p::X28p& acc, const uint8_t* __restrict__ part
         zany |= w[28 + i];
     }
     // the identity is zz = 0 on both lanes (pair-uniform predicate)
+    if (!r28p::both(zany == 0)) r28p::xadd(acc, x, y, zz, zzz);
+}
+MBLS_DEV void xadd_raw(r28p::X28p& acc, const uint32_t (&w)[56]) {
+    r28::F28 x, y, zz, zzz;
+    uint32_t zany = 0;
+#pragma unroll
+    for (int i = 0; i < 14; ++i) {
+        x.l[i] = w[i];
+        y.l[i] = w[14 + i];
+        zz.l[i] = w[28 + i];
+        zzz.l[i] = w[42 + i];
+        zany |= w[28 + i];
+    }
     if (!r28p::both(zany == 0)) r28p::xadd(acc, x, y, zz, zzz);
 }
 // pair XYZZ sum -> the library's Jacobian words of this lane's component
@@ -884,14 +905,16 @@ MBLS_DEV bool load_j28(const uint8_t* __restrict__ base, size_t i, r28::F28& x, 
 }
 // r28 XYZZ addition of chunk partial k (G1 with MBLS_ACC_XYZZ: the light path's and the slice
 // chains' form; raw limbs, store_xyzz28); the identity (zz = 0) adds nothing
-MBLS_DEV void r28_add_partial(r28::X28& acc, const uint8_t* __restrict__ partials, uint32_t k) {
-    const uint4* q = reinterpret_cast<const uint4*>(partials + (size_t)k * 224);
-    uint32_t w[56];
+// the 56 raw words of XYZZ record k (224 B; `half` selects the odd lane's half of a 448-B pair record)
+MBLS_DEV void load_raw56(const uint8_t* __restrict__ recs, size_t off, uint32_t (&w)[56]) {
+    const uint4* q = reinterpret_cast<const uint4*>(recs + off);
 #pragma unroll
     for (int j = 0; j < 14; ++j) {
         const uint4 u = q[j];
         w[4 * j] = u.x, w[4 * j + 1] = u.y, w[4 * j + 2] = u.z, w[4 * j + 3] = u.w;
     }
+}
+MBLS_DEV void xadd_raw(r28::X28& acc, const uint32_t (&w)[56]) {
     r28::F28 x, y, zz, zzz;
     uint32_t zany = 0;
 #pragma unroll
@@ -903,6 +926,11 @@ MBLS_DEV void r28_add_partial(r28::X28& acc, const uint8_t* __restrict__ partial
         zany |= w[28 + i];
     }
     if (zany) r28::xadd(acc, x, y, zz, zzz);
+}
+MBLS_DEV void r28_add_partial(r28::X28& acc, const uint8_t* __restrict__ partials, uint32_t k) {
+    uint32_t w[56];
+    load_raw56(partials, (size_t)k * 224, w);
+    xadd_raw(acc, w);
 }
 // r28 lane addition of Jacobian chunk partial k (G1 without MBLS_ACC_XYZZ)
 MBLS_DEV void r28_add_partial(r28::J28& acc, const uint8_t* __restrict__ partials, uint32_t k) {
@@ -944,7 +972,7 @@ static constexpr uint32_t HEAVY_SLICE_MIN = MBLS_HEAVY_SLICE_MIN, HEAVY_LDS = 10
 // (X, Y, Z^2, Z^3) the lane-mode level 0 reads (k_reduce_scaled_r28x).  Wave 0, all 64 lanes.
 template <class F>
 MBLS_DEV void store_bucket_row(uint8_t* __restrict__ buckets, uint32_t b, const RJac<F>& p, bool xb) {
-    if constexpr (buckets_xyzz_ok<F>()) {
+    if constexpr (std::is_same<F, Fq>::value && buckets_xyzz_ok<F>()) {
         if (xb) {
             uint32_t w[3][12], zany = 0;
 #pragma unroll
@@ -964,6 +992,32 @@ MBLS_DEV void store_bucket_row(uint8_t* __restrict__ buckets, uint32_t b, const 
                 a.zzz = r28::mul(a.zz, z);
             }
             store_xyzz28(buckets, b, a);
+            return;
+        }
+    }
+    if constexpr (std::is_same<F, Fq2>::value && buckets_xyzz_ok<F>()) {
+        if (xb) {  // every lane of wave 0 forms its pair component (c0 on even lanes, c1 on odd)
+            const bool odd = pairdpp::odd();
+            uint32_t w[3][12], zany = 0;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+                const uint32_t x0 = (uint32_t)__shfl((int)p.x.c0.v, i, 64), x1 = (uint32_t)__shfl((int)p.x.c1.v, i, 64);
+                const uint32_t y0 = (uint32_t)__shfl((int)p.y.c0.v, i, 64), y1 = (uint32_t)__shfl((int)p.y.c1.v, i, 64);
+                const uint32_t z0 = (uint32_t)__shfl((int)p.z.c0.v, i, 64), z1 = (uint32_t)__shfl((int)p.z.c1.v, i, 64);
+                w[0][i] = odd ? x1 : x0;
+                w[1][i] = odd ? y1 : y0;
+                w[2][i] = odd ? z1 : z0;
+                zany |= z0 | z1;
+            }
+            r28p::X28p a = r28p::X28p::inf();
+            if (zany) {  // wave-uniform
+                const r28::F28 z = r28::fold(r28::unpack_shift8(w[2]));
+                a.x = r28::fold(r28::unpack_shift8(w[0]));
+                a.y = r28::fold(r28::unpack_shift8(w[1]));
+                a.zz = r28p::sqr<r28::B16>(z);
+                a.zzz = r28p::mul<r28::B16>(a.zz, z);
+            }
+            if (threadIdx.x < 2) store_xyzz28p(buckets, b, a);
             return;
         }
     }
@@ -1201,7 +1255,10 @@ __global__ __launch_bounds__(256, MBLS_BS_MINW) void k_bucket_small(const uint32
         // pair-sliced radix-2^28 XYZZ sums of the raw XYZZ partials (round 6), one conversion
         r28p::X28p acc = r28p::X28p::inf();
         for (uint32_t k = k0; k < k1; ++k) r28p_add_partial(acc, partials, k);
-        store_jac<L>(buckets, b, xyzz28p_to_words(acc));
+        if (xb)
+            store_xyzz28p(buckets, b, acc);
+        else
+            store_jac<L>(buckets, b, xyzz28p_to_words(acc));
         return;
     }
     Jacobian<L> acc = Jacobian<L>::inf();
@@ -1293,6 +1350,9 @@ __global__ __launch_bounds__(256) void k_reduce_scaled_r28(const uint8_t* __rest
     store_jac28(Uout, tid, S);
 }
 
+#ifndef MBLS_RED0_PREFETCH
+#define MBLS_RED0_PREFETCH 1  // level 0 loads bucket t - 1 before adding bucket t
+#endif
 // level 0 over raw XYZZ buckets (buckets_xyzz_ok, no U): the chain of k_reduce_scaled_r28 with
 // add-2008-s (r28::xadd, 12M + 2S) for its two additions per step, the outputs converted once
 template <class F>  // F = Fq only
@@ -1309,15 +1369,57 @@ __global__ __launch_bounds__(256) void k_reduce_scaled_r28x(const uint8_t* __res
     const uint32_t k1 = min(k0 + seg, m_in);  // exclusive
     const uint32_t base = w * m_in;
     r28::X28 R = r28::X28::inf(), S = r28::X28::inf();
+    uint32_t nw[56];  // bucket t - 1, loaded while bucket t is added (one wave per SIMD: nothing else hides it)
+    load_raw56(V, (size_t)(base + k1 - 1) * 224, nw);
     for (uint32_t t = k1; t-- > k0;) {
-        r28_add_partial(R, V, base + t);                                                   // R += V_t
+        uint32_t cw[56];
+#pragma unroll
+        for (int i = 0; i < 56; ++i) cw[i] = nw[i];
+        if (MBLS_RED0_PREFETCH && t > k0) load_raw56(V, (size_t)(base + t - 1) * 224, nw);
+        xadd_raw(R, cw);                                                                   // R += V_t
         if ((t - k0) + off != 0 && !R.is_inf()) r28::xadd(S, R.x, R.y, R.zz, R.zzz);  // S += R
+        if (!MBLS_RED0_PREFETCH && t > k0) load_raw56(V, (size_t)(base + t - 1) * 224, nw);
     }
     if (Vout) {
         for (uint32_t k = 0; k < seg_log; ++k) r28::xdbl(R);
         store_jac28(Vout, tid, r28::x_to_jac(R));
     }
     store_jac28(Uout, tid, r28::x_to_jac(S));
+}
+
+// the same over raw pair-sliced XYZZ buckets (G2): one chain per lane pair, outputs in Jacobian
+// words (store_jac<PFq2>, the form the next level reads)
+template <class F>  // F = Fq2 only
+__global__ __launch_bounds__(256) void k_reduce_scaled_r28px(const uint8_t* __restrict__ V, uint32_t m_in,
+                                                             uint32_t seg_log, int Wg, int off,
+                                                             uint8_t* __restrict__ Vout, uint8_t* __restrict__ Uout) {
+    MBLS_TAIL_PRIO();
+    const uint32_t seg = 1u << seg_log;
+    const uint32_t m_out = (m_in + seg - 1) >> seg_log;
+    const uint32_t tid = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // pair-uniform
+    if (tid >= m_out * (uint32_t)Wg) return;
+    const uint32_t w = tid / m_out, q = tid % m_out;
+    const uint32_t k0 = q << seg_log;
+    const uint32_t k1 = min(k0 + seg, m_in);  // exclusive
+    const uint32_t base = w * m_in;
+    r28p::X28p R = r28p::X28p::inf(), S = r28p::X28p::inf();
+    const size_t half = pairdpp::odd() ? 224 : 0;
+    uint32_t nw[56];
+    load_raw56(V, (size_t)(base + k1 - 1) * 448 + half, nw);
+    for (uint32_t t = k1; t-- > k0;) {
+        uint32_t cw[56];
+#pragma unroll
+        for (int i = 0; i < 56; ++i) cw[i] = nw[i];
+        if (MBLS_RED0_PREFETCH && t > k0) load_raw56(V, (size_t)(base + t - 1) * 448 + half, nw);
+        xadd_raw(R, cw);                                                                    // R += V_t
+        if ((t - k0) + off != 0 && !R.is_inf()) r28p::xadd(S, R.x, R.y, R.zz, R.zzz);  // S += R
+        if (!MBLS_RED0_PREFETCH && t > k0) load_raw56(V, (size_t)(base + t - 1) * 448 + half, nw);
+    }
+    if (Vout) {
+        for (uint32_t k = 0; k < seg_log; ++k) r28p::xdbl(R);
+        store_jac<PFq2>(Vout, tid, xyzz28p_to_words(R));
+    }
+    store_jac<PFq2>(Uout, tid, xyzz28p_to_words(S));
 }
 
 // A narrow level (few segments: the GPU is idle but for one wave per chain) as a tree: one
@@ -1858,7 +1960,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     const size_t NC = P.contributions;
     const uint32_t max_chunks = (uint32_t)(NC / P.chunk + TB + 1);
     const bool xb = buckets_xyzz<F>(P);
-    MsmScratchSizes z = msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value, xb ? 224 : JAC);
+    MsmScratchSizes z =
+        msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value, xb ? xyzz_bucket_bytes<F>() : JAC);
     uint32_t* keys = (uint32_t*)arena.take(z.keys);
     uint32_t* vals = (uint32_t*)arena.take(z.vals);
     uint32_t* ranks = (uint32_t*)arena.take(z.ranks);
@@ -2025,8 +2128,13 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             bool done = false;
             if constexpr (buckets_xyzz_ok<F>()) {
                 if (l == 0 && xb) {
-                    hipLaunchKernelGGL((k_reduce_scaled_r28x<F>), dim3((m_out * (uint32_t)P.Wg + 255) / 256), dim3(256),
-                                       0, st, V, m_in, P.seg_log[0], P.Wg, 1, Vo, Uo);
+                    const uint32_t chains = m_out * (uint32_t)P.Wg;
+                    if constexpr (std::is_same<F, Fq>::value)
+                        hipLaunchKernelGGL((k_reduce_scaled_r28x<F>), dim3((chains + 255) / 256), dim3(256), 0, st, V,
+                                           m_in, P.seg_log[0], P.Wg, 1, Vo, Uo);
+                    else
+                        hipLaunchKernelGGL((k_reduce_scaled_r28px<F>), dim3((2 * chains + 255) / 256), dim3(256), 0, st,
+                                           V, m_in, P.seg_log[0], P.Wg, 1, Vo, Uo);
                     done = true;
                 }
             }
@@ -2119,7 +2227,9 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
                 P.c, P.W, P.Wg, P.split, P.TB, P.contributions, P.chunk, P.levels);
     uint32_t max_chunks = (uint32_t)(P.contributions / P.chunk + P.TB + 1);
     size_t scratch =
-        msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value, buckets_xyzz<F>(P) ? 224 : JAC).total();
+        msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value,
+                          buckets_xyzz<F>(P) ? xyzz_bucket_bytes<F>() : JAC)
+            .total();
     const bool piped = batch > 1 && batch_pipe() > 0;
     er = lease.reserve(st_s + st_b + st_r + scratch * (piped ? 2 : 1) + 4096);
     if (er != MBLS_SUCCESS) return er;

@@ -399,6 +399,24 @@ def test_msm_adversarial_heavy_buckets(amd, gh, c):
     assert gh.decode_icicle("g1", out[0]) == H.g1_from_affine_mont(ref)
 
 
+def test_msm_g2_heavy_buckets_raw_xyzz_level0(amd, gh):
+    """G2 at c = 16 (4 psi windows of 2^15 buckets: reduction level 0 in lanes, so the bucket sums
+    stay raw pair-sliced XYZZ): all scalars equal (one heavy bucket per window, summed by slice
+    workgroups and converted from the row layout) and random scalars (light buckets), vs the oracle."""
+    import torch
+    n = 1 << 12
+    b = torch.zeros((n, 24), dtype=torch.int64, device="cuda")
+    amd.gen_bases("g2", b, 77)
+    bn = amd.to_numpy_u64(b)
+    s_one = H.ints_to_limbs([pr.R - 54321] * n, 4)
+    out = amd.msm("g2", amd.torch_u64(s_one), b, icicle=True, c=16, n=n)
+    assert gh.decode_icicle("g2", out[0]) == H.g2_from_affine_mont(H.oracle_msm("g2", s_one, bn))
+    s = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    amd.gen_scalars(s, 4321)
+    out = amd.msm("g2", s, b, icicle=True, c=16, n=n)
+    assert gh.decode_icicle("g2", out[0]) == H.g2_from_affine_mont(H.oracle_msm("g2", amd.to_numpy_u64(s), bn))
+
+
 @pytest.mark.parametrize("group", ["g1", "g2"])
 def test_msm_chunk_start_exceptional_pairs(amd, gh, group):
     """the accumulation adds a chunk's second point with the affine + affine formula (its first
