@@ -1381,18 +1381,21 @@ __global__ __launch_bounds__(256) void k_reduce_scaled_r28x(const uint8_t* __res
         if (!MBLS_RED0_PREFETCH && t > k0) load_raw56(V, (size_t)(base + t - 1) * 224, nw);
     }
     if (Vout) {
-        for (uint32_t k = 0; k < seg_log; ++k) r28::xdbl(R);
+        if (!R.is_inf())
+            for (uint32_t k = 0; k < seg_log; ++k) r28::xdbl(R);
         store_jac28(Vout, tid, r28::x_to_jac(R));
     }
     store_jac28(Uout, tid, r28::x_to_jac(S));
 }
 
-// the same over raw pair-sliced XYZZ buckets (G2): one chain per lane pair, outputs in Jacobian
-// words (store_jac<PFq2>, the form the next level reads)
+// the same over raw pair-sliced XYZZ records (G2): one chain per lane pair; a lane level after
+// level 0 adds U_t too (raw, from the previous lane level).  Outputs raw when the next level is a
+// lane level too (raw_out), else Jacobian words (store_jac<PFq2>, the form a row / wave level reads)
 template <class F>  // F = Fq2 only
-__global__ __launch_bounds__(256) void k_reduce_scaled_r28px(const uint8_t* __restrict__ V, uint32_t m_in,
-                                                             uint32_t seg_log, int Wg, int off,
-                                                             uint8_t* __restrict__ Vout, uint8_t* __restrict__ Uout) {
+__global__ __launch_bounds__(256) void k_reduce_scaled_r28px(const uint8_t* __restrict__ V, const uint8_t* __restrict__ U,
+                                                             uint32_t m_in, uint32_t seg_log, int Wg, int off,
+                                                             uint8_t* __restrict__ Vout, uint8_t* __restrict__ Uout,
+                                                             int raw_out) {
     MBLS_TAIL_PRIO();
     const uint32_t seg = 1u << seg_log;
     const uint32_t m_out = (m_in + seg - 1) >> seg_log;
@@ -1414,12 +1417,25 @@ __global__ __launch_bounds__(256) void k_reduce_scaled_r28px(const uint8_t* __re
         xadd_raw(R, cw);                                                                    // R += V_t
         if ((t - k0) + off != 0 && !R.is_inf()) r28p::xadd(S, R.x, R.y, R.zz, R.zzz);  // S += R
         if (!MBLS_RED0_PREFETCH && t > k0) load_raw56(V, (size_t)(base + t - 1) * 448 + half, nw);
+        if (U) {  // S += U_t
+            load_raw56(U, (size_t)(base + t) * 448 + half, cw);
+            xadd_raw(S, cw);
+        }
     }
     if (Vout) {
-        for (uint32_t k = 0; k < seg_log; ++k) r28p::xdbl(R);
-        store_jac<PFq2>(Vout, tid, xyzz28p_to_words(R));
+        // the identity stays exactly zz = 0: a pair product by zz = 0 is only 0 mod p (the partner's
+        // negation is a bias multiple of p), which a raw record would carry on as a point
+        if (!R.is_inf())
+            for (uint32_t k = 0; k < seg_log; ++k) r28p::xdbl(R);
+        if (raw_out)
+            store_xyzz28p(Vout, tid, R);
+        else
+            store_jac<PFq2>(Vout, tid, xyzz28p_to_words(R));
     }
-    store_jac<PFq2>(Uout, tid, xyzz28p_to_words(S));
+    if (raw_out)
+        store_xyzz28p(Uout, tid, S);
+    else
+        store_jac<PFq2>(Uout, tid, xyzz28p_to_words(S));
 }
 
 // A narrow level (few segments: the GPU is idle but for one wave per chain) as a tree: one
@@ -1783,9 +1799,20 @@ template <class F>
 inline bool buckets_xyzz(const MsmPlan& P) {
     return buckets_xyzz_ok<F>() && P.levels > 0 && P.mode[0] == MODE_LANE;
 }
+#ifndef MBLS_RED_RAW_G2
+#define MBLS_RED_RAW_G2 1  // G2 lane levels after level 0 take raw pair XYZZ records from the level before
+#endif
+// a level output record's bytes: raw pair XYZZ (448) when G2 chains lane levels, else Jacobian
+template <class F>
+inline size_t level_bytes(const MsmPlan& P, size_t jac) {
+    return (std::is_same<F, Fq2>::value && MBLS_RED_RAW_G2 && buckets_xyzz<F>(P) && P.levels > 1 &&
+            P.mode[1] == MODE_LANE)
+               ? xyzz_bucket_bytes<F>()
+               : jac;
+}
 // bkt: a bucket sum's bytes (jac, or 224 for raw XYZZ buckets)
 inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t aff, uint32_t max_chunks, size_t part,
-                                         size_t bkt) {
+                                         size_t bkt, size_t lvl) {
     MsmScratchSizes z;
     // the per-call image table; with bstride > 1 also the compact copy of the points (2n rows)
     z.phi = P.split > 1 && !P.prepared ? align_up(P.pts / P.split * (P.split - 1 + (P.bstride > 1 ? 1 : 0)) * aff) : 0;
@@ -1828,8 +1855,8 @@ inline MsmScratchSizes msm_scratch_sizes(const MsmPlan& P, size_t jac, size_t af
     z.buckets = align_up((size_t)P.TB * bkt);
     // V / U ping-pong halves sized for the widest level's outputs (k_reduce_scaled)
     const size_t mo0 = P.levels ? (P.level_m[0] + P.seg(0) - 1) / P.seg(0) : 1;
-    z.levelT = align_up(2 * mo0 * P.Wg * jac);
-    z.levelR = align_up(2 * mo0 * P.Wg * jac);
+    z.levelT = align_up(2 * mo0 * P.Wg * lvl);  // lvl: a level record's bytes (level_bytes)
+    z.levelR = align_up(2 * mo0 * P.Wg * lvl);
     z.windows = align_up((size_t)P.Wg * jac);
     return z;
 }
@@ -1961,7 +1988,8 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
     const uint32_t max_chunks = (uint32_t)(NC / P.chunk + TB + 1);
     const bool xb = buckets_xyzz<F>(P);
     MsmScratchSizes z =
-        msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value, xb ? xyzz_bucket_bytes<F>() : JAC);
+        msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value, xb ? xyzz_bucket_bytes<F>() : JAC,
+                          level_bytes<F>(P, JAC));
     uint32_t* keys = (uint32_t*)arena.take(z.keys);
     uint32_t* vals = (uint32_t*)arena.take(z.vals);
     uint32_t* ranks = (uint32_t*)arena.take(z.ranks);
@@ -2114,11 +2142,12 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
         ProfScope ps_red("msm.reduce", st);  // the levels only (k_final has its own scope)
         // scaled running-sum levels (k_reduce_scaled): V / U ping-pong in levelR / levelT, the
         // last level writes the window sums straight into `windows`
-        const size_t half = ((P.level_m[0] + P.seg(0) - 1) / P.seg(0)) * (size_t)P.Wg * JAC;
+        const size_t half = ((P.level_m[0] + P.seg(0) - 1) / P.seg(0)) * (size_t)P.Wg * level_bytes<F>(P, JAC);
         uint8_t* vb[2] = {levelR, levelR + half};
         uint8_t* ub[2] = {levelT, levelT + half};
         const uint8_t* V = buckets;
         const uint8_t* U = nullptr;
+        bool raw_in = xb;  // level l's inputs are raw XYZZ records
         for (int l = 0; l < P.levels; ++l) {
             const uint32_t m_in = P.level_m[l];
             const uint32_t m_out = (m_in + P.seg(l) - 1) / P.seg(l);
@@ -2127,14 +2156,18 @@ eIcicleError msm_device(const uint8_t* scalars, bool scalars_mont, const uint8_t
             uint8_t* Uo = last ? windows : ub[l & 1];
             bool done = false;
             if constexpr (buckets_xyzz_ok<F>()) {
-                if (l == 0 && xb) {
+                if (raw_in) {  // a lane level (level 0, or G2's lane levels after it)
                     const uint32_t chains = m_out * (uint32_t)P.Wg;
-                    if constexpr (std::is_same<F, Fq>::value)
+                    if constexpr (std::is_same<F, Fq>::value) {
                         hipLaunchKernelGGL((k_reduce_scaled_r28x<F>), dim3((chains + 255) / 256), dim3(256), 0, st, V,
                                            m_in, P.seg_log[0], P.Wg, 1, Vo, Uo);
-                    else
+                        raw_in = false;
+                    } else {
+                        const bool raw_out = MBLS_RED_RAW_G2 && !last && P.mode[l + 1] == MODE_LANE;
                         hipLaunchKernelGGL((k_reduce_scaled_r28px<F>), dim3((2 * chains + 255) / 256), dim3(256), 0, st,
-                                           V, m_in, P.seg_log[0], P.Wg, 1, Vo, Uo);
+                                           V, U, m_in, P.seg_log[l], P.Wg, l == 0 ? 1 : 0, Vo, Uo, raw_out ? 1 : 0);
+                        raw_in = raw_out;
+                    }
                     done = true;
                 }
             }
@@ -2228,7 +2261,7 @@ eIcicleError msm_call(const void* scalars, const void* bases, int msm_size, cons
     uint32_t max_chunks = (uint32_t)(P.contributions / P.chunk + P.TB + 1);
     size_t scratch =
         msm_scratch_sizes(P, JAC, AFF, max_chunks, PartialBytes<F>::value,
-                          buckets_xyzz<F>(P) ? xyzz_bucket_bytes<F>() : JAC)
+                          buckets_xyzz<F>(P) ? xyzz_bucket_bytes<F>() : JAC, level_bytes<F>(P, JAC))
             .total();
     const bool piped = batch > 1 && batch_pipe() > 0;
     er = lease.reserve(st_s + st_b + st_r + scratch * (piped ? 2 : 1) + 4096);
